@@ -1,0 +1,163 @@
+/*
+ * wq4.h -- C ABI of the MI355X-native fused Q4_0 dequant + GEMM path.
+ *
+ * Drop-in boundary for the reference's Q4 operator surface
+ * (zerr0o/whisper-burn, src/gguf/{tensor,op,linear}.rs, src/model/layers.rs).
+ * Every entry point names the reference item it replaces (file:line).  The
+ * reference binds this path in-process through Burn/CubeCL; a Rust maintainer
+ * would bind these symbols with `extern "C"`.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  `stream` is a hipStream_t passed as
+ *    void* (NULL = the device's null stream).  Device pointers (`*_dev`) are
+ *    hipMalloc'd memory on the tensor's device.
+ *  - Shapes follow the reference: weights [N, K] = [out_features, in_features]
+ *    (tensor.rs:29-33), activations [B, M, K] f32 contiguous, outputs
+ *    [B, M, N] f32 contiguous (op.rs:41-46, :73).
+ *  - Every call returns a wq4_status; on failure wq4_last_error() returns a
+ *    thread-local message.  Nothing aborts (the reference panics at
+ *    op.rs:53,58-61,106 -- here those are WQ4_ESHAPE / WQ4_EHIP).
+ *  - Calls are stream-ordered and asynchronous: no implicit device sync, no
+ *    allocation inside the *_ws entry points (graph-capturable).  Distinct
+ *    streams may be used concurrently from distinct host threads.
+ *  - Result precision: products are formed from f16 hi/lo splits of the f32
+ *    activations (x = hi + lo, both f16, ~22 significant bits) against the
+ *    exact f16 value (q - 8) of each nibble, accumulated in f32 by MFMA; the
+ *    per-block f16 scale is applied in f32 (see DESIGN.md "Numerics").
+ */
+#ifndef WQ4_H
+#define WQ4_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WQ4_ABI_VERSION 1
+
+typedef enum wq4_status {
+  WQ4_OK = 0,
+  WQ4_EINVAL = 1,      /* null pointer / bad argument                         */
+  WQ4_ESHAPE = 2,      /* shape rule violated (tensor.rs:38-42, op.rs:53-61) */
+  WQ4_EBYTES = 3,      /* byte count != N*K/32*18 (tensor.rs:43-48)          */
+  WQ4_EHIP = 4,        /* HIP runtime error (launch, memcpy, malloc)         */
+  WQ4_ENOMEM = 5,      /* workspace too small / allocation failed            */
+  WQ4_EUNSUPPORTED = 6 /* valid request this build does not implement        */
+} wq4_status;
+
+/* Activation precision of the product (see header comment).             */
+typedef enum wq4_precision {
+  WQ4_PREC_F16X2 = 0, /* default: x = hi + lo, two f16 MFMA passes           */
+  WQ4_PREC_F16 = 1    /* fast: x rounded to f16, one MFMA pass               */
+} wq4_precision;
+
+/* Epilogue flags for the *_ex entry points.                              */
+#define WQ4_EPI_GELU 1u     /* tanh-GELU after bias (layers.rs:35-41)       */
+#define WQ4_EPI_RESIDUAL 2u /* y = residual + (x W^T + b); residual may == y */
+
+typedef struct wq4_tensor wq4_tensor; /* Q4Tensor (src/gguf/tensor.rs:21-27) */
+
+/* ---- library -------------------------------------------------------- */
+const char* wq4_last_error(void);
+int wq4_abi_version(void);
+wq4_status wq4_device_count(int* count);
+/* Process-wide default precision for calls that do not pass one. */
+wq4_status wq4_set_precision(wq4_precision prec);
+wq4_precision wq4_get_precision(void);
+
+/* ---- Q4Tensor (src/gguf/tensor.rs) ------------------------------------ */
+/* Q4Tensor::from_q4_bytes (tensor.rs:35-71).  `raw` = host bytes exactly as
+ * stored in GGUF: N*K/32 blocks of 18 B (f16 scale LE, 16 nibble bytes; low
+ * nibble = elements 0..15, high = 16..31).  Errors: WQ4_ESHAPE if N*K % 32
+ * (tensor.rs:38-42) or, additionally to the reference, K % 32 (the shader
+ * needs it, shader.wgsl:69, but Q4Tensor never checks); WQ4_EBYTES if nbytes
+ * != N*K/32*18 (tensor.rs:43-48).  The bytes are repacked on upload into the
+ * MFMA fragment order (lossless; wq4_tensor_raw_bytes returns them again). */
+wq4_status wq4_tensor_create(int device, const uint8_t* raw, size_t nbytes, int64_t n, int64_t k,
+                             wq4_tensor** out);
+void wq4_tensor_destroy(wq4_tensor* t);
+/* Q4Tensor::shape (tensor.rs:74-76): [N, K]. */
+wq4_status wq4_tensor_shape(const wq4_tensor* t, int64_t* n, int64_t* k);
+/* Q4Tensor::num_blocks (tensor.rs:79-81). */
+int64_t wq4_tensor_num_blocks(const wq4_tensor* t);
+int wq4_tensor_device(const wq4_tensor* t);
+/* Q4Tensor::dequantize (tensor.rs:88-113): D2H read then host dequant into
+ * `host_out` [N*K] f32 (synchronous, diagnostics only, as in the reference). */
+wq4_status wq4_tensor_dequantize(const wq4_tensor* t, float* host_out);
+/* D2H read of the device copy, un-repacked to the original GGUF bytes
+ * [N*K/32*18] (synchronous; proves the repack is lossless). */
+wq4_status wq4_tensor_raw_bytes(const wq4_tensor* t, uint8_t* host_out);
+/* Bytes of device memory the tensor holds. */
+size_t wq4_tensor_device_bytes(const wq4_tensor* t);
+
+/* ---- q4_matmul (src/gguf/op.rs:47-117) ---------------------------------- */
+/* y[B,M,N] = x[B,M,K] . W[N,K]^T.  x_dev, y_dev: f32 device buffers on the
+ * tensor's device.  K must equal W's K (op.rs:58-61).  Uses an internal,
+ * grow-only per-device workspace (allocation happens only on growth). */
+wq4_status wq4_matmul(const wq4_tensor* w, const float* x_dev, float* y_dev, int64_t b, int64_t m, int64_t k,
+                      void* stream);
+
+/* Q4Linear::forward (src/gguf/linear.rs:34-40): y = x W^T (+ bias[N]).
+ * bias_dev may be NULL (cross-attention key has none, loader.rs:205-210). */
+wq4_status wq4_linear_forward(const wq4_tensor* w, const float* bias_dev, const float* x_dev, float* y_dev,
+                              int64_t b, int64_t m, int64_t k, void* stream);
+
+/* Q4FFN::forward (src/model/layers.rs:54-58): y = fc2(gelu(fc1(x))), with
+ * the GELU fused into fc1's epilogue and the intermediate kept in the
+ * MFMA operand layout (never materialised as f32). */
+wq4_status wq4_ffn_forward(const wq4_tensor* fc1, const float* b1_dev, const wq4_tensor* fc2,
+                           const float* b2_dev, const float* x_dev, float* y_dev, int64_t b, int64_t m,
+                           void* stream);
+
+/* ---- explicit-workspace / extended forms (graph-capturable) ----------- */
+/* Workspace bytes needed by wq4_linear_forward_ws for these sizes. */
+size_t wq4_linear_workspace_bytes(const wq4_tensor* w, int64_t rows);
+/* Workspace bytes needed by wq4_ffn_forward_ws. */
+size_t wq4_ffn_workspace_bytes(const wq4_tensor* fc1, const wq4_tensor* fc2, int64_t rows);
+/* y = epi(x W^T + bias); flags = WQ4_EPI_*; residual_dev used iff
+ * WQ4_EPI_RESIDUAL (may alias y_dev).  rows = B*M.  No allocation. */
+wq4_status wq4_linear_forward_ws(const wq4_tensor* w, const float* bias_dev, const float* x_dev,
+                                 const float* residual_dev, float* y_dev, int64_t rows, int64_t k,
+                                 unsigned flags, wq4_precision prec, void* workspace, size_t ws_bytes,
+                                 void* stream);
+wq4_status wq4_ffn_forward_ws(const wq4_tensor* fc1, const float* b1_dev, const wq4_tensor* fc2,
+                              const float* b2_dev, const float* x_dev, const float* residual_dev, float* y_dev,
+                              int64_t rows, unsigned flags, wq4_precision prec, void* workspace,
+                              size_t ws_bytes, void* stream);
+
+/* ---- operand-layout entry points (producers that emit A-tiled) -------- */
+/* Bytes of an A-tiled operand buffer for `rows` x `k` activations.       */
+size_t wq4_atiled_bytes(int64_t rows, int64_t k, wq4_precision prec);
+/* f32 [rows, k] (row stride ld floats) -> A-tiled operand (f16 hi[/lo]).  */
+wq4_status wq4_tile_activations(const float* x_dev, int64_t rows, int64_t k, int64_t ld, wq4_precision prec,
+                                void* at_dev, size_t at_bytes, void* stream);
+/* y = epi(A W^T + bias) from an A-tiled operand (no conversion pass).     */
+wq4_status wq4_linear_forward_tiled(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
+                                    const float* residual_dev, float* y_dev, int64_t rows, unsigned flags,
+                                    wq4_precision prec, void* stream);
+/* Same, writing the result as the A-tiled operand of a following GEMM whose
+ * K equals this N (used for fc1 -> fc2; bias/GELU applied first).          */
+wq4_status wq4_linear_forward_tiled_out(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
+                                        void* at_out_dev, size_t at_out_bytes, int64_t rows, unsigned flags,
+                                        wq4_precision prec, void* stream);
+
+/* ---- kernel selection (exposed for tests and the bench) -------------- */
+/* 0 = automatic (by rows), 1 = force the MFMA tile kernel ("prefill"),
+ * 2 = force the K-split streaming kernel ("decode").  Both compute each
+ * output row with an M-independent instruction sequence. */
+wq4_status wq4_set_kernel_policy(int policy);
+
+/* ---- host-only diagnostics (no GPU needed) ---------------------------- */
+/* Sizes of the repacked nibble / scale arrays for a [N, K] tensor. */
+wq4_status wq4_debug_repacked_bytes(int64_t n, int64_t k, size_t* nib_bytes, size_t* sc_bytes);
+/* The repack wq4_tensor_create applies on upload, run on the host. */
+wq4_status wq4_debug_repack(const uint8_t* raw, int64_t n, int64_t k, uint8_t* nib_out, uint32_t* sc_out);
+/* Its inverse (raw GGUF bytes from the repacked arrays). */
+wq4_status wq4_debug_unrepack(const uint8_t* nib, const uint32_t* sc, int64_t n, int64_t k, uint8_t* raw_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WQ4_H */

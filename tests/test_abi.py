@@ -1,0 +1,120 @@
+"""C-ABI library tests that need no GPU: load, exports, host logic, errors.
+
+No compute call is made here (there is no GPU in the build container); the
+shape / byte-count validation of Q4Tensor::from_q4_bytes (tensor.rs:38-48)
+runs before any device work, so its error behaviour is testable on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+import wq4
+
+
+def test_library_loads_and_reports_abi():
+    L = wq4.lib()
+    assert L.wq4_abi_version() == 1
+
+
+def test_every_header_function_is_exported():
+    L = wq4.lib()
+    names = wq4.header_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_no_oracle_symbols_in_product():
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--defined-only", wq4.LIB_PATH], capture_output=True, text=True).stdout
+    assert "q4o_" not in out  # the product never contains the checker
+
+
+@pytest.mark.parametrize("n,k", [(1, 32), (32, 32), (64, 128), (96, 64), (1280, 1280), (33, 96), (5120, 160)])
+def test_repack_roundtrip_lossless(n, k):
+    rng = np.random.default_rng(n * 7 + k)
+    raw = rng.integers(0, 256, n * k // 32 * 18, dtype=np.uint8)
+    nib, sc = wq4.debug_repack(raw, n, k)
+    assert nib.size == ((n + 63) // 64 * 2) * ((k // 32 + 1) // 2) * 1024
+    back = wq4.debug_unrepack(nib, sc, n, k)
+    assert np.array_equal(back, raw)
+    # same information content: 4.5 bits per weight + padding only
+    assert nib.size + sc.size * 4 >= raw.size
+
+
+def test_repack_layout_spec():
+    """Spot-check wq4_layout.hpp: lane (r, h) of (n-tile, block pair) holds the
+    kk=0/1 nibble words of bytes 8h..8h+7 of row 32*nt + r, blocks 2bp, 2bp+1."""
+    n, k = 64, 128
+    w = oracle.closed_form(1, n * k)
+    raw = oracle.quantize_convert_np(w)
+    nib, sc = wq4.debug_repack(raw, n, k)
+    nbp = 2
+    words = nib.view(np.uint32).reshape(2, nbp, 64, 4)
+    blocks = raw.reshape(n, k // 32, 18)
+    for nt in range(2):
+        for bp in range(nbp):
+            for lane in (0, 5, 31, 32, 63):
+                r, h = lane & 31, lane >> 5
+                for bi in range(2):
+                    blk = blocks[32 * nt + r, 2 * bp + bi]
+                    by = blk[2 + 8 * h: 10 + 8 * h]
+                    for kk in range(2):
+                        q = [(b >> 4) if kk else (b & 15) for b in by]
+                        want = sum(int(q[2 * i]) << (4 * i) | int(q[2 * i + 1]) << (16 + 4 * i) for i in range(4))
+                        assert words[nt, bp, lane, bi * 2 + kk] == want
+                    d = int(blk[0]) | int(blk[1]) << 8
+                    assert (int(sc.reshape(2, nbp, 32)[nt, bp, r]) >> (16 * bi)) & 0xFFFF == d
+
+
+def test_deq8_arithmetic_is_exact():
+    """The kernel's nibble -> f16 (q - 8) trick, in numpy f16: exact for all q."""
+    q = np.arange(16, dtype=np.uint16)
+    lo = (np.uint16(0x6400) | q).view(np.float16)
+    hi = (np.uint16(0x6400) | (q << 4)).view(np.float16)
+    a = (lo - np.float16(1032)).astype(np.float32)
+    b = (hi * np.float16(0.0625) - np.float16(72)).astype(np.float32)
+    assert np.array_equal(a, q.astype(np.float32) - 8) and np.array_equal(b, q.astype(np.float32) - 8)
+
+
+def _create(raw, n, k):
+    h = ctypes.c_void_p(None)
+    st = wq4.lib().wq4_tensor_create(0, raw.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), raw.size, n, k,
+                                     ctypes.byref(h))
+    return st, wq4.lib().wq4_last_error().decode()
+
+
+def test_create_rejects_bad_element_count():
+    """tensor.rs:38-42 message."""
+    raw = np.zeros(18, np.uint8)
+    st, msg = _create(raw, 3, 5)
+    assert st == 2 and "divisible by 32, got 15" in msg
+
+
+def test_create_rejects_bad_byte_count():
+    """tensor.rs:43-48 message."""
+    raw = np.zeros(17, np.uint8)
+    st, msg = _create(raw, 1, 32)
+    assert st == 3 and "expected 18 for 1 blocks, got 17" in msg
+
+
+def test_create_rejects_partial_block_rows():
+    raw = np.zeros(18, np.uint8)
+    st, msg = _create(raw, 2, 16)  # 32 elements but K % 32 != 0
+    assert st == 2 and "K % 32" in msg
+
+
+def test_precision_and_policy_setters():
+    wq4.set_precision(wq4.PREC_F16)
+    assert wq4.get_precision() == wq4.PREC_F16
+    wq4.set_precision(wq4.PREC_F16X2)
+    with pytest.raises(wq4.WQ4Error):
+        wq4.set_precision(7)
+    with pytest.raises(wq4.WQ4Error):
+        wq4.set_kernel_policy(9)
+    wq4.set_kernel_policy(0)

@@ -1,0 +1,340 @@
+"""GPU parity tests of the fused Q4_0 dequant+GEMM (run on an MI355X).
+
+Each of the reference's 9 GPU tests (src/gguf/tests.rs) is re-expressed with
+its own inputs and tolerance, calling the HIP kernels through the C ABI, and
+then tightened: every result is also compared with a float64 evaluation of
+the same dequantized product, against the error bound of the f16-hi/lo
+scheme (DESIGN.md "Numerics"):
+
+    |y_gpu - y_f64| <= TOL_REL * sum_k |x_k w_k| + TOL_ABS * sum_k |w_k|
+
+TOL_REL = 4e-6, TOL_ABS = 2^-24 for WQ4_PREC_F16X2 (x split into two f16
+terms, ~22 significant bits; f32 MFMA accumulation), and TOL_REL = 6e-4 for
+WQ4_PREC_F16.  For scale: the reference's own f32 loop (tests.rs:172-184) is
+bounded only by K * 2^-24 * sum|x w| (6e-5 at K = 1280).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle
+import wq4
+
+pytestmark = pytest.mark.gpu
+
+TOL = {wq4.PREC_F16X2: (4e-6, 2.0**-24), wq4.PREC_F16: (6e-4, 2.0**-12)}
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as _t
+
+    assert _t.cuda.is_available(), "GPU tests need an MI355X"
+    assert wq4.device_count() >= 1
+    return _t
+
+
+@pytest.fixture(autouse=True)
+def _reset_modes():
+    wq4.set_precision(wq4.PREC_F16X2)
+    wq4.set_kernel_policy(0)
+    yield
+    wq4.set_precision(wq4.PREC_F16X2)
+    wq4.set_kernel_policy(0)
+
+
+def to_dev(torch, a, shape):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32).reshape(shape)).to("cuda:0")
+
+
+def assert_q4_close(y, x2d, deq2d, prec=wq4.PREC_F16X2, bias=None, what=""):
+    truth, mag = oracle.matmul_f64(x2d, deq2d)
+    if bias is not None:
+        truth = truth + np.asarray(bias, np.float64)[None, :]
+    wabs = np.abs(np.asarray(deq2d, np.float64)).sum(axis=1)[None, :]
+    rel, ab = TOL[prec]
+    bound = rel * mag + ab * wabs + 1e-30 + (0 if bias is None else 2**-24 * np.abs(truth))
+    err = np.abs(np.asarray(y, np.float64).reshape(truth.shape) - truth)
+    worst = float(np.max(err / bound))
+    assert worst <= 1.0, f"{what}: max err/bound = {worst:.3g} (max err {err.max():.3g})"
+    return worst
+
+
+def make_weights(n, k, kind=1):
+    w = oracle.closed_form(kind, n * k)
+    q = oracle.quantize_test(w)
+    return q, oracle.dequantize_np(q, n * k).reshape(n, k)
+
+
+# ------------------------------------------------------- reference tests --
+def test_q4_dequantize_gpu(torch):
+    """tests.rs:331-363 (< 1e-5; here bit-exact)."""
+    x = oracle.closed_form(4, 256)
+    q = oracle.quantize_test(x)
+    t = wq4.Q4Tensor.from_q4_bytes(q, [16, 16])
+    deq = t.dequantize()
+    assert list(deq.shape) == [16, 16]
+    want = oracle.dequantize_c(q, 256).reshape(16, 16)
+    assert np.array_equal(deq.cpu().numpy(), want)
+
+
+def test_q4_matmul_small(torch):
+    """tests.rs:370-410: 32x32, act i*0.1, vs reference_matmul, < 1e-3."""
+    k = n = 32
+    q, deq = make_weights(n, k, kind=2)
+    act = oracle.closed_form(3, k)
+    expected = oracle.reference_matmul(act, deq.ravel(), 1, k, n)
+    t = wq4.Q4Tensor.from_q4_bytes(q, [n, k])
+    out = wq4.q4_matmul(to_dev(torch, act, (1, 1, k)), t)
+    assert list(out.shape) == [1, 1, n]
+    y = out.cpu().numpy().reshape(1, n)
+    assert np.max(np.abs(y - expected)) < 1e-3
+    assert_q4_close(y, act.reshape(1, k), deq, what="small")
+
+
+SHAPES = [(1, 1, 128, 64), (1, 1, 1280, 1280), (1, 10, 1280, 1280), (1, 1, 1280, 5120), (1, 1, 5120, 1280)]
+
+
+@pytest.mark.parametrize("batch,seq,k,n", SHAPES)
+@pytest.mark.parametrize("policy", [0, 1, 2])
+def test_q4_matmul_shapes(torch, batch, seq, k, n, policy):
+    """tests.rs:413-480 (tol 1e-2 vs f32 matmul), both kernels."""
+    wq4.set_kernel_policy(policy)
+    act = oracle.closed_form(0, batch * seq * k)
+    q, deq = make_weights(n, k, kind=1)
+    expected = oracle.reference_matmul(act, deq.ravel(), batch * seq, k, n)
+    t = wq4.Q4Tensor.from_q4_bytes(q, [n, k])
+    out = wq4.q4_matmul(to_dev(torch, act, (batch, seq, k)), t)
+    assert list(out.shape) == [batch, seq, n]
+    y = out.cpu().numpy().reshape(batch * seq, n)
+    assert np.max(np.abs(y - expected)) < 1e-2
+    assert_q4_close(y, act.reshape(-1, k), deq, what=f"{(batch, seq, k, n)} policy {policy}")
+
+
+def test_q4_linear_forward_shape(torch):
+    """tests.rs:487-506."""
+    q, _ = make_weights(64, 128, kind=0)
+    lin = wq4.Q4Linear(wq4.Q4Tensor.from_q4_bytes(q, [64, 128]), None)
+    out = lin.forward(torch.zeros((2, 5, 128), dtype=torch.float32, device="cuda:0"))
+    assert list(out.shape) == [2, 5, 64]
+    assert torch.count_nonzero(out).item() == 0
+
+
+def test_q4_linear_forward_with_bias(torch):
+    """tests.rs:509-564 (< 1e-3 vs reference matmul + bias)."""
+    q, deq = make_weights(32, 64, kind=0)
+    bias = oracle.closed_form(8, 32)
+    lin = wq4.Q4Linear(wq4.Q4Tensor.from_q4_bytes(q, [32, 64]), to_dev(torch, bias, (32,)))
+    act = oracle.closed_form(3, 64)
+    out = lin.forward(to_dev(torch, act, (1, 1, 64)))
+    assert list(out.shape) == [1, 1, 32]
+    expected = oracle.reference_matmul(act, deq.ravel(), 1, 64, 32) + bias
+    y = out.cpu().numpy().reshape(1, 32)
+    assert np.max(np.abs(y - expected)) < 1e-3
+    assert_q4_close(y, act.reshape(1, 64), deq, bias=bias, what="bias")
+
+
+def test_q4_ffn_forward_shape(torch):
+    """tests.rs:571-597 (shape only, zero input) -- plus zero output."""
+    d, f = 64, 256
+    q1, _ = make_weights(f, d, kind=7)
+    q2, _ = make_weights(d, f, kind=7)
+    ffn = wq4.Q4FFN(wq4.Q4Linear(wq4.Q4Tensor.from_q4_bytes(q1, [f, d])),
+                    wq4.Q4Linear(wq4.Q4Tensor.from_q4_bytes(q2, [d, f])))
+    out = ffn.forward(torch.zeros((1, 4, d), dtype=torch.float32, device="cuda:0"))
+    assert list(out.shape) == [1, 4, d]
+    assert torch.count_nonzero(out).item() == 0  # gelu(0) = 0, no bias
+
+
+def test_q4_matmul_batch(torch):
+    """tests.rs:604-655: (4, 10, 128, 64), < 1e-3."""
+    b, s, k, n = 4, 10, 128, 64
+    act = oracle.closed_form(0, b * s * k)
+    q, deq = make_weights(n, k, kind=1)
+    out = wq4.q4_matmul(to_dev(torch, act, (b, s, k)), wq4.Q4Tensor.from_q4_bytes(q, [n, k]))
+    y = out.cpu().numpy().reshape(b * s, n)
+    expected = oracle.shader_matmul(q, act, b, s, k, n).reshape(b * s, n)
+    assert np.max(np.abs(y - expected)) < 1e-3
+    assert_q4_close(y, act.reshape(-1, k), deq, what="batch")
+
+
+def test_q4_roundtrip_small(torch):
+    """tests.rs:662-706: device dequant == CPU dequant; raw bytes survive."""
+    x = oracle.closed_form(5, 32 * 64)
+    q = oracle.quantize_test(x)
+    t = wq4.Q4Tensor.from_q4_bytes(q, [32, 64])
+    gpu = t.dequantize().cpu().numpy().ravel()
+    assert np.array_equal(gpu, oracle.dequantize_c(q, x.size))
+    assert np.max(np.abs(gpu - x)) < 0.1
+    assert np.array_equal(t.raw_bytes(), q)
+    assert t.num_blocks() == 64 and t.shape() == [32, 64]
+
+
+def test_q4_matmul_encoder_shape(torch):
+    """tests.rs:713-764: (1, 32, 1280, 1280), < 1e-2."""
+    act = oracle.closed_form(0, 32 * 1280)
+    q, deq = make_weights(1280, 1280, kind=1)
+    out = wq4.q4_matmul(to_dev(torch, act, (1, 32, 1280)), wq4.Q4Tensor.from_q4_bytes(q, [1280, 1280]))
+    y = out.cpu().numpy().reshape(32, 1280)
+    assert np.max(np.abs(y - oracle.reference_matmul(act, deq.ravel(), 32, 1280, 1280))) < 1e-2
+    assert_q4_close(y, act.reshape(32, 1280), deq, what="encoder32")
+
+
+# --------------------------------------------- beyond the reference tests --
+WHISPER = [  # (N, K): Large-V3 and Medium projections and FFN
+    (1280, 1280), (5120, 1280), (1280, 5120), (1024, 1024), (4096, 1024), (1024, 4096)]
+
+
+@pytest.mark.parametrize("n,k", WHISPER)
+@pytest.mark.parametrize("m", [1, 4, 32, 1500])
+def test_whisper_shapes_reference_quantizer(torch, n, k, m):
+    """Real Whisper shapes (full M = 1500 encoder rows), weights quantized by
+    the product quantizer (convert_whisper.py), random activations."""
+    rng = np.random.default_rng(n + 3 * k + m)
+    w = (rng.standard_normal(n * k) * 0.02).astype(np.float32)
+    q = oracle.quantize_convert_np(w)
+    deq = oracle.dequantize_np(q, n * k).reshape(n, k)
+    x = rng.standard_normal(m * k).astype(np.float32)
+    t = wq4.Q4Tensor.from_q4_bytes(q, [n, k])
+    y = wq4.q4_matmul(to_dev(torch, x, (1, m, k)), t).cpu().numpy().reshape(m, n)
+    assert_q4_close(y, x.reshape(m, k), deq, what=f"{(m, n, k)}")
+
+
+@pytest.mark.parametrize("policy", [1, 2])
+def test_batch_invariance(torch, policy):
+    """Rows of a batch-of-clips call equal the single-clip call bit for bit
+    (the per-row K-reduction order never depends on M or on the tile)."""
+    wq4.set_kernel_policy(policy)
+    n, k = 1280, 1280
+    rng = np.random.default_rng(11)
+    q = oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.02).astype(np.float32))
+    t = wq4.Q4Tensor.from_q4_bytes(q, [n, k])
+    m1 = 1500 if policy == 1 else 1
+    nb = 3 if policy == 1 else 32
+    x = rng.standard_normal(nb * m1 * k).astype(np.float32)
+    xb = to_dev(torch, x, (nb, m1, k))
+    yb = wq4.q4_matmul(xb, t).cpu().numpy()
+    for i in (0, nb - 1):
+        yi = wq4.q4_matmul(xb[i:i + 1].contiguous(), t).cpu().numpy()
+        assert np.array_equal(yb[i:i + 1].view(np.uint32), yi.view(np.uint32))
+
+
+def test_prefill_and_decode_kernels_agree(torch):
+    n, k, m = 5120, 1280, 48
+    rng = np.random.default_rng(5)
+    q = oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.02).astype(np.float32))
+    t = wq4.Q4Tensor.from_q4_bytes(q, [n, k])
+    x = to_dev(torch, rng.standard_normal(m * k).astype(np.float32), (1, m, k))
+    wq4.set_kernel_policy(1)
+    a = wq4.q4_matmul(x, t).cpu().numpy()
+    wq4.set_kernel_policy(2)
+    b = wq4.q4_matmul(x, t).cpu().numpy()
+    deq = oracle.dequantize_np(q, n * k).reshape(n, k)
+    assert_q4_close(a.reshape(m, n), x.cpu().numpy().reshape(m, k), deq, what="prefill")
+    assert_q4_close(b.reshape(m, n), x.cpu().numpy().reshape(m, k), deq, what="decode")
+
+
+@pytest.mark.parametrize("policy", [1, 2])
+def test_precision_f16_mode(torch, policy):
+    wq4.set_kernel_policy(policy)
+    wq4.set_precision(wq4.PREC_F16)
+    n, k, m = 1280, 1280, 64
+    rng = np.random.default_rng(6)
+    q = oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.02).astype(np.float32))
+    deq = oracle.dequantize_np(q, n * k).reshape(n, k)
+    x = rng.standard_normal(m * k).astype(np.float32)
+    y = wq4.q4_matmul(to_dev(torch, x, (1, m, k)), wq4.Q4Tensor.from_q4_bytes(q, [n, k])).cpu().numpy()
+    assert_q4_close(y.reshape(m, n), x.reshape(m, k), deq, prec=wq4.PREC_F16, what="f16")
+
+
+@pytest.mark.parametrize("n,k", [(32, 32), (96, 64), (64, 96), (33 * 32, 160), (100, 320)])
+@pytest.mark.parametrize("m", [1, 5, 65, 130])
+def test_ragged_shapes(torch, n, k, m):
+    """Odd block counts, N not a multiple of 64, M not a multiple of 32/64."""
+    rng = np.random.default_rng(n * k + m)
+    q = oracle.quantize_convert_np(rng.uniform(-1, 1, n * k).astype(np.float32))
+    deq = oracle.dequantize_np(q, n * k).reshape(n, k)
+    x = rng.standard_normal(m * k).astype(np.float32)
+    for policy in (1, 2):
+        wq4.set_kernel_policy(policy)
+        y = wq4.q4_matmul(to_dev(torch, x, (1, m, k)), wq4.Q4Tensor.from_q4_bytes(q, [n, k])).cpu().numpy()
+        assert_q4_close(y.reshape(m, n), x.reshape(m, k), deq, what=f"ragged {(m, n, k)} p{policy}")
+
+
+def test_activation_range_edges(torch):
+    """f16 subnormal lo terms (tiny x) and large |x| (up to ~4e4)."""
+    n, k, m = 256, 512, 8
+    rng = np.random.default_rng(9)
+    q = oracle.quantize_convert_np(rng.uniform(-1, 1, n * k).astype(np.float32))
+    deq = oracle.dequantize_np(q, n * k).reshape(n, k)
+    for scale in (1e-6, 1e-3, 1e4):  # f16 hi term: |x| < 65504
+        x = (rng.standard_normal(m * k) * scale).astype(np.float32)
+        x[::97] = 0.0
+        y = wq4.q4_matmul(to_dev(torch, x, (1, m, k)), wq4.Q4Tensor.from_q4_bytes(q, [n, k])).cpu().numpy()
+        assert_q4_close(y.reshape(m, n), x.reshape(m, k), deq, what=f"scale {scale}")
+
+
+def test_zero_rows_is_noop(torch):
+    q, _ = make_weights(64, 128)
+    t = wq4.Q4Tensor.from_q4_bytes(q, [64, 128])
+    out = wq4.q4_matmul(torch.zeros((0, 3, 128), dtype=torch.float32, device="cuda:0"), t)
+    assert list(out.shape) == [0, 3, 64]
+
+
+def test_k_mismatch_raises(torch):
+    """op.rs:58-61 panics; the C ABI returns WQ4_ESHAPE with the same text."""
+    q, _ = make_weights(64, 128)
+    t = wq4.Q4Tensor.from_q4_bytes(q, [64, 128])
+    with pytest.raises(wq4.WQ4Error, match="K dimension mismatch: input has 96, weights have 128"):
+        wq4.q4_matmul(torch.zeros((1, 1, 96), dtype=torch.float32, device="cuda:0"), t)
+
+
+@pytest.mark.parametrize("policy", [1, 2])
+def test_ffn_numerics_vs_oracle(torch, policy):
+    """Q4FFN numerics -- unpinned in the reference (shape-only test); here vs
+    the oracle's layers.rs:35-58 restatement in float64 with f32 GELU."""
+    wq4.set_kernel_policy(policy)
+    d, f, m = 1280, 5120, 40
+    rng = np.random.default_rng(12)
+    q1 = oracle.quantize_convert_np((rng.standard_normal(f * d) * 0.02).astype(np.float32))
+    q2 = oracle.quantize_convert_np((rng.standard_normal(d * f) * 0.02).astype(np.float32))
+    b1 = (rng.standard_normal(f) * 0.01).astype(np.float32)
+    b2 = (rng.standard_normal(d) * 0.01).astype(np.float32)
+    x = rng.standard_normal(m * d).astype(np.float32)
+    ffn = wq4.Q4FFN(wq4.Q4Linear(wq4.Q4Tensor.from_q4_bytes(q1, [f, d]), to_dev(torch, b1, (f,))),
+                    wq4.Q4Linear(wq4.Q4Tensor.from_q4_bytes(q2, [d, f]), to_dev(torch, b2, (d,))))
+    y = ffn.forward(to_dev(torch, x, (1, m, d))).cpu().numpy().reshape(m, d)
+    w1 = oracle.dequantize_np(q1, f * d).reshape(f, d).astype(np.float64)
+    w2 = oracle.dequantize_np(q2, d * f).reshape(d, f).astype(np.float64)
+    h = x.reshape(m, d).astype(np.float64) @ w1.T + b1
+    g = oracle.gelu_np(h.astype(np.float32)).astype(np.float64)
+    want = g @ w2.T + b2
+    mag = np.abs(g) @ np.abs(w2).T + 1.0
+    err = np.abs(y - want)
+    assert np.max(err / mag) < 2e-5, np.max(err / mag)
+
+
+def test_linear_ws_residual_and_gelu(torch):
+    """The fused epilogue flags of wq4_linear_forward_ws: y = res + gelu(xW^T+b)."""
+    import ctypes
+
+    n, k, m = 1280, 1280, 100
+    rng = np.random.default_rng(13)
+    q = oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.02).astype(np.float32))
+    deq = oracle.dequantize_np(q, n * k).reshape(n, k)
+    t = wq4.Q4Tensor.from_q4_bytes(q, [n, k])
+    x = to_dev(torch, rng.standard_normal(m * k).astype(np.float32), (m, k))
+    b = to_dev(torch, (rng.standard_normal(n) * 0.1).astype(np.float32), (n,))
+    res = to_dev(torch, rng.standard_normal(m * n).astype(np.float32), (m, n))
+    y = res.clone()
+    nbytes = wq4.lib().wq4_linear_workspace_bytes(t.handle, m)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+    wq4.check(wq4.lib().wq4_linear_forward_ws(t.handle, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                              ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(y.data_ptr()), m, k,
+                                              wq4.EPI_GELU | wq4.EPI_RESIDUAL, wq4.PREC_F16X2,
+                                              ctypes.c_void_p(ws.data_ptr()), nbytes,
+                                              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    h = x.cpu().numpy().astype(np.float64) @ deq.T.astype(np.float64) + b.cpu().numpy()
+    want = res.cpu().numpy() + oracle.gelu_np(h.astype(np.float32))
+    assert np.max(np.abs(y.cpu().numpy() - want)) < 1e-4

@@ -1,0 +1,470 @@
+// wq4_api.cpp -- C ABI (include/wq4.h) over the MI355X Q4_0 kernels.
+//
+// Mirrors the reference operator surface:
+//   Q4Tensor::{from_q4_bytes, shape, num_blocks, dequantize}  src/gguf/tensor.rs
+//   q4_matmul                                                 src/gguf/op.rs:47-117
+//   Q4Linear::forward                                         src/gguf/linear.rs:34-40
+//   Q4FFN::forward (+ gelu)                                   src/model/layers.rs:35-58
+// Differences by design: no hidden per-call uploads (op.rs:67-70 uploads an
+// info buffer and flushes the queue on every call), caller-owned outputs,
+// status codes instead of panics.
+#include <hip/hip_runtime_api.h>
+
+#include <cstdio>
+#include <cstring>
+#include <atomic>
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/wq4.h"
+#include "wq4_kernels.hpp"
+#include "wq4_layout.hpp"
+
+struct wq4_tensor {
+  int device = 0;
+  wq4::Q4Geom g;
+  uint8_t* nib = nullptr;   // device, g.nib_bytes()
+  uint32_t* sc = nullptr;   // device, g.sc_bytes()
+};
+
+namespace {
+
+thread_local std::string g_err;
+std::atomic<int> g_prec{WQ4_PREC_F16X2};
+std::atomic<int> g_policy{0};
+
+wq4_status fail(wq4_status s, const std::string& msg) {
+  g_err = msg;
+  return s;
+}
+
+wq4_status hip_fail(hipError_t e, const char* what) {
+  return fail(WQ4_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// RAII device switch (hipSetDevice is per host thread).
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// Grow-only workspace per (device, stream) for the convenience entry points.
+struct Arena {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_arena_mu;
+std::map<std::pair<int, void*>, Arena> g_arenas;
+
+wq4_status arena_get(int dev, void* stream, size_t need, void** out) {
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  Arena& a = g_arenas[{dev, stream}];
+  if (a.bytes < need) {
+    if (a.ptr) {
+      // pending work on this stream may still read the old buffer
+      hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+      if (e != hipSuccess) return hip_fail(e, "arena sync");
+      (void)hipFree(a.ptr);
+      a.ptr = nullptr;
+      a.bytes = 0;
+    }
+    size_t sz = need < ((size_t)1 << 20) ? ((size_t)1 << 20) : need;
+    hipError_t e = hipMalloc(&a.ptr, sz);
+    if (e != hipSuccess) return fail(WQ4_ENOMEM, std::string("workspace hipMalloc: ") + hipGetErrorString(e));
+    a.bytes = sz;
+  }
+  *out = a.ptr;
+  return WQ4_OK;
+}
+
+int ns_of(wq4_precision p) { return p == WQ4_PREC_F16 ? 1 : 2; }
+
+bool use_decode(int64_t rows) {
+  const int pol = g_policy.load();
+  if (pol == 1) return false;
+  if (pol == 2) return true;
+  return rows <= 64;
+}
+
+wq4::EpiArgs make_epi(const float* bias, const float* residual, float* out, int ldo, int m, int n, bool gelu) {
+  wq4::EpiArgs e{};
+  e.bias = bias;
+  e.residual = residual;
+  e.out = out;
+  e.out_tiled = nullptr;
+  e.ldo = ldo;
+  e.nbp_next = 0;
+  e.gelu = gelu ? 1 : 0;
+  e.m = m;
+  e.n = n;
+  return e;
+}
+
+wq4_status check_prec(wq4_precision p) {
+  if (p != WQ4_PREC_F16X2 && p != WQ4_PREC_F16) return fail(WQ4_EINVAL, "unknown precision");
+  return WQ4_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* wq4_last_error(void) { return g_err.c_str(); }
+int wq4_abi_version(void) { return WQ4_ABI_VERSION; }
+
+wq4_status wq4_device_count(int* count) {
+  if (!count) return fail(WQ4_EINVAL, "count is null");
+  hipError_t e = hipGetDeviceCount(count);
+  if (e != hipSuccess) {
+    *count = 0;
+    return hip_fail(e, "hipGetDeviceCount");
+  }
+  return WQ4_OK;
+}
+
+wq4_status wq4_set_precision(wq4_precision prec) {
+  wq4_status s = check_prec(prec);
+  if (s != WQ4_OK) return s;
+  g_prec.store(prec);
+  return WQ4_OK;
+}
+
+wq4_precision wq4_get_precision(void) { return static_cast<wq4_precision>(g_prec.load()); }
+
+wq4_status wq4_set_kernel_policy(int policy) {
+  if (policy < 0 || policy > 2) return fail(WQ4_EINVAL, "policy must be 0, 1 or 2");
+  g_policy.store(policy);
+  return WQ4_OK;
+}
+
+// Q4Tensor::from_q4_bytes, src/gguf/tensor.rs:35-71.
+wq4_status wq4_tensor_create(int device, const uint8_t* raw, size_t nbytes, int64_t n, int64_t k,
+                             wq4_tensor** out) {
+  if (!out) return fail(WQ4_EINVAL, "out is null");
+  *out = nullptr;
+  if (n <= 0 || k <= 0) return fail(WQ4_ESHAPE, "Q4_0 shape must be positive, got [" + std::to_string(n) + ", " +
+                                                    std::to_string(k) + "]");
+  const int64_t elems = n * k;
+  if (elems % 32 != 0)  // tensor.rs:38-42
+    return fail(WQ4_ESHAPE, "Q4_0 requires element count divisible by 32, got " + std::to_string(elems));
+  if (k % 32 != 0)  // shader.wgsl:69 assumes it; the reference never checks
+    return fail(WQ4_ESHAPE, "Q4_0 rows must hold whole blocks: K % 32 != 0 (K = " + std::to_string(k) + ")");
+  const int64_t nblocks = elems / 32;
+  const size_t expected = (size_t)nblocks * 18;
+  if (nbytes != expected)  // tensor.rs:43-48
+    return fail(WQ4_EBYTES, "Q4_0 byte count mismatch: expected " + std::to_string(expected) + " for " +
+                                std::to_string(nblocks) + " blocks, got " + std::to_string(nbytes));
+  if (!raw) return fail(WQ4_EINVAL, "raw is null");
+  if (n > (1 << 24) || k > (1 << 24)) return fail(WQ4_ESHAPE, "dimension too large for this build (> 2^24)");
+
+  DeviceGuard dg(device);
+  if (!dg.ok) return fail(WQ4_EHIP, "hipSetDevice(" + std::to_string(device) + ") failed");
+  auto* t = new wq4_tensor();
+  t->device = device;
+  t->g = wq4::make_geom(n, k);
+  std::vector<uint8_t> nib(t->g.nib_bytes());
+  std::vector<uint32_t> sc(t->g.sc_bytes() / 4);
+  wq4::repack_q4(raw, t->g, nib.data(), sc.data());
+  hipError_t e = hipMalloc(&t->nib, nib.size());
+  if (e == hipSuccess) e = hipMalloc(&t->sc, t->g.sc_bytes());
+  if (e == hipSuccess) e = hipMemcpy(t->nib, nib.data(), nib.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(t->sc, sc.data(), t->g.sc_bytes(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    wq4_tensor_destroy(t);
+    return hip_fail(e, "Q4Tensor upload");
+  }
+  *out = t;
+  return WQ4_OK;
+}
+
+void wq4_tensor_destroy(wq4_tensor* t) {
+  if (!t) return;
+  DeviceGuard dg(t->device);
+  if (t->nib) (void)hipFree(t->nib);
+  if (t->sc) (void)hipFree(t->sc);
+  delete t;
+}
+
+wq4_status wq4_tensor_shape(const wq4_tensor* t, int64_t* n, int64_t* k) {
+  if (!t || !n || !k) return fail(WQ4_EINVAL, "null argument");
+  *n = t->g.n;
+  *k = t->g.k;
+  return WQ4_OK;
+}
+
+int64_t wq4_tensor_num_blocks(const wq4_tensor* t) { return t ? t->g.n * t->g.kb : -1; }
+int wq4_tensor_device(const wq4_tensor* t) { return t ? t->device : -1; }
+size_t wq4_tensor_device_bytes(const wq4_tensor* t) { return t ? t->g.nib_bytes() + t->g.sc_bytes() : 0; }
+
+wq4_status wq4_tensor_raw_bytes(const wq4_tensor* t, uint8_t* host_out) {
+  if (!t || !host_out) return fail(WQ4_EINVAL, "null argument");
+  DeviceGuard dg(t->device);
+  std::vector<uint8_t> nib(t->g.nib_bytes());
+  std::vector<uint32_t> sc(t->g.sc_bytes() / 4);
+  hipError_t e = hipMemcpy(nib.data(), t->nib, nib.size(), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(sc.data(), t->sc, t->g.sc_bytes(), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "Q4Tensor read-back");
+  wq4::unrepack_q4(nib.data(), sc.data(), t->g, host_out);
+  return WQ4_OK;
+}
+
+static float f16_to_f32_host(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+
+// Q4Tensor::dequantize, src/gguf/tensor.rs:88-113 (D2H, then host dequant).
+wq4_status wq4_tensor_dequantize(const wq4_tensor* t, float* host_out) {
+  if (!t || !host_out) return fail(WQ4_EINVAL, "null argument");
+  std::vector<uint8_t> raw((size_t)t->g.n * t->g.kb * 18);
+  wq4_status s = wq4_tensor_raw_bytes(t, raw.data());
+  if (s != WQ4_OK) return s;
+  const int64_t nb = t->g.n * t->g.kb;
+  for (int64_t b = 0; b < nb; ++b) {
+    const uint8_t* o = raw.data() + b * 18;
+    const float d = f16_to_f32_host((uint16_t)(o[0] | (o[1] << 8)));
+    float* dst = host_out + b * 32;
+    for (int i = 0; i < 16; ++i) {
+      const float lo = (float)(o[2 + i] & 0x0f) - 8.0f;
+      const float hi = (float)((o[2 + i] >> 4) & 0x0f) - 8.0f;
+      dst[i] = lo * d;
+      dst[i + 16] = hi * d;
+    }
+  }
+  return WQ4_OK;
+}
+
+size_t wq4_linear_workspace_bytes(const wq4_tensor* w, int64_t rows) {
+  if (!w) return 0;
+  return wq4::atiled_bytes(rows, w->g.k, 2);
+}
+
+size_t wq4_ffn_workspace_bytes(const wq4_tensor* fc1, const wq4_tensor* fc2, int64_t rows) {
+  if (!fc1 || !fc2) return 0;
+  return wq4::atiled_bytes(rows, fc1->g.k, 2) + wq4::atiled_bytes(rows, fc2->g.k, 2);
+}
+
+static wq4_status linear_impl(const wq4_tensor* w, const float* bias, const float* x, const float* residual,
+                              float* y, int64_t rows, int64_t k, unsigned flags, wq4_precision prec, void* ws,
+                              size_t ws_bytes, void* stream) {
+  if (!w || !x || !y) return fail(WQ4_EINVAL, "null argument");
+  wq4_status s = check_prec(prec);
+  if (s != WQ4_OK) return s;
+  if (k != w->g.k)  // op.rs:58-61
+    return fail(WQ4_ESHAPE, "K dimension mismatch: input has " + std::to_string(k) + ", weights have " +
+                                std::to_string(w->g.k));
+  if (rows < 0 || rows > (1 << 24)) return fail(WQ4_ESHAPE, "bad row count " + std::to_string(rows));
+  if ((flags & WQ4_EPI_RESIDUAL) && !residual) return fail(WQ4_EINVAL, "WQ4_EPI_RESIDUAL without residual");
+  if (rows == 0) return WQ4_OK;
+  const int ns = ns_of(prec);
+  const size_t need = wq4::atiled_bytes(rows, k, ns);
+  if (!ws || ws_bytes < need)
+    return fail(WQ4_ENOMEM, "workspace too small: need " + std::to_string(need) + " bytes");
+  DeviceGuard dg(w->device);
+  if (!dg.ok) return fail(WQ4_EHIP, "hipSetDevice failed");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto* at = static_cast<_Float16*>(ws);
+  hipError_t e = wq4::launch_tile_activations(x, at, (int)rows, (int)k, (int)k, ns, st);
+  if (e != hipSuccess) return hip_fail(e, "tile_activations launch");
+  wq4::EpiArgs epi = make_epi(bias, (flags & WQ4_EPI_RESIDUAL) ? residual : nullptr, y, (int)w->g.n, (int)rows,
+                              (int)w->g.n, (flags & WQ4_EPI_GELU) != 0);
+  e = wq4::launch_q4_gemm(w->g, w->nib, w->sc, at, (int)rows, epi, wq4::kEpiF32, ns, use_decode(rows), st);
+  if (e != hipSuccess) return hip_fail(e, "q4_gemm launch");
+  return WQ4_OK;
+}
+
+wq4_status wq4_linear_forward_ws(const wq4_tensor* w, const float* bias_dev, const float* x_dev,
+                                 const float* residual_dev, float* y_dev, int64_t rows, int64_t k, unsigned flags,
+                                 wq4_precision prec, void* workspace, size_t ws_bytes, void* stream) {
+  return linear_impl(w, bias_dev, x_dev, residual_dev, y_dev, rows, k, flags, prec, workspace, ws_bytes, stream);
+}
+
+wq4_status wq4_linear_forward(const wq4_tensor* w, const float* bias_dev, const float* x_dev, float* y_dev,
+                              int64_t b, int64_t m, int64_t k, void* stream) {
+  if (!w) return fail(WQ4_EINVAL, "weights are null");
+  if (b < 0 || m < 0) return fail(WQ4_ESHAPE, "negative B or M");
+  const int64_t rows = b * m;
+  const wq4_precision prec = wq4_get_precision();
+  void* ws = nullptr;
+  const size_t need = wq4::atiled_bytes(rows, k, ns_of(prec));
+  {
+    DeviceGuard dg(w->device);
+    wq4_status s = arena_get(w->device, stream, need, &ws);
+    if (s != WQ4_OK) return s;
+  }
+  return linear_impl(w, bias_dev, x_dev, nullptr, y_dev, rows, k, 0u, prec, ws, need, stream);
+}
+
+// q4_matmul, src/gguf/op.rs:47-117.
+wq4_status wq4_matmul(const wq4_tensor* w, const float* x_dev, float* y_dev, int64_t b, int64_t m, int64_t k,
+                      void* stream) {
+  return wq4_linear_forward(w, nullptr, x_dev, y_dev, b, m, k, stream);
+}
+
+static wq4_status ffn_impl(const wq4_tensor* fc1, const float* b1, const wq4_tensor* fc2, const float* b2,
+                           const float* x, const float* residual, float* y, int64_t rows, unsigned flags,
+                           wq4_precision prec, void* ws, size_t ws_bytes, void* stream) {
+  if (!fc1 || !fc2 || !x || !y) return fail(WQ4_EINVAL, "null argument");
+  wq4_status s = check_prec(prec);
+  if (s != WQ4_OK) return s;
+  if (fc1->device != fc2->device) return fail(WQ4_EINVAL, "fc1 and fc2 live on different devices");
+  if (fc2->g.k != fc1->g.n)
+    return fail(WQ4_ESHAPE, "FFN shape mismatch: fc1 is [" + std::to_string(fc1->g.n) + ", " +
+                                std::to_string(fc1->g.k) + "], fc2 is [" + std::to_string(fc2->g.n) + ", " +
+                                std::to_string(fc2->g.k) + "]");
+  if ((flags & WQ4_EPI_RESIDUAL) && !residual) return fail(WQ4_EINVAL, "WQ4_EPI_RESIDUAL without residual");
+  if (rows < 0 || rows > (1 << 24)) return fail(WQ4_ESHAPE, "bad row count");
+  if (rows == 0) return WQ4_OK;
+  const int ns = ns_of(prec);
+  const size_t n1 = wq4::atiled_bytes(rows, fc1->g.k, ns);
+  const size_t n2 = wq4::atiled_bytes(rows, fc2->g.k, ns);
+  if (!ws || ws_bytes < n1 + n2) return fail(WQ4_ENOMEM, "workspace too small: need " + std::to_string(n1 + n2));
+  DeviceGuard dg(fc1->device);
+  if (!dg.ok) return fail(WQ4_EHIP, "hipSetDevice failed");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto* a1 = static_cast<_Float16*>(ws);
+  auto* a2 = reinterpret_cast<_Float16*>(static_cast<uint8_t*>(ws) + n1);
+  const bool dec = use_decode(rows);
+  hipError_t e = wq4::launch_tile_activations(x, a1, (int)rows, (int)fc1->g.k, (int)fc1->g.k, ns, st);
+  if (e != hipSuccess) return hip_fail(e, "tile_activations launch");
+  // fc1 + bias + GELU, written straight into fc2's operand layout.
+  wq4::EpiArgs e1 = make_epi(b1, nullptr, nullptr, (int)fc1->g.n, (int)rows, (int)fc1->g.n, true);
+  e1.out_tiled = a2;
+  e1.nbp_next = (int)fc2->g.nbp;
+  e = wq4::launch_q4_gemm(fc1->g, fc1->nib, fc1->sc, a1, (int)rows, e1, wq4::kEpiTiled, ns, dec, st);
+  if (e != hipSuccess) return hip_fail(e, "fc1 launch");
+  wq4::EpiArgs e2 = make_epi(b2, (flags & WQ4_EPI_RESIDUAL) ? residual : nullptr, y, (int)fc2->g.n, (int)rows,
+                             (int)fc2->g.n, (flags & WQ4_EPI_GELU) != 0);
+  e = wq4::launch_q4_gemm(fc2->g, fc2->nib, fc2->sc, a2, (int)rows, e2, wq4::kEpiF32, ns, dec, st);
+  if (e != hipSuccess) return hip_fail(e, "fc2 launch");
+  return WQ4_OK;
+}
+
+wq4_status wq4_ffn_forward_ws(const wq4_tensor* fc1, const float* b1_dev, const wq4_tensor* fc2,
+                              const float* b2_dev, const float* x_dev, const float* residual_dev, float* y_dev,
+                              int64_t rows, unsigned flags, wq4_precision prec, void* workspace, size_t ws_bytes,
+                              void* stream) {
+  return ffn_impl(fc1, b1_dev, fc2, b2_dev, x_dev, residual_dev, y_dev, rows, flags, prec, workspace, ws_bytes,
+                  stream);
+}
+
+size_t wq4_atiled_bytes(int64_t rows, int64_t k, wq4_precision prec) {
+  if (rows < 0 || k <= 0 || k % 32 != 0) return 0;
+  return wq4::atiled_bytes(rows, k, ns_of(prec));
+}
+
+wq4_status wq4_tile_activations(const float* x_dev, int64_t rows, int64_t k, int64_t ld, wq4_precision prec,
+                                void* at_dev, size_t at_bytes, void* stream) {
+  wq4_status s = check_prec(prec);
+  if (s != WQ4_OK) return s;
+  if (!x_dev || !at_dev) return fail(WQ4_EINVAL, "null argument");
+  if (rows < 0 || rows > (1 << 24) || k <= 0 || k % 32 != 0 || ld < k)
+    return fail(WQ4_ESHAPE, "bad activation shape");
+  if (at_bytes < wq4::atiled_bytes(rows, k, ns_of(prec))) return fail(WQ4_ENOMEM, "A-tiled buffer too small");
+  hipError_t e = wq4::launch_tile_activations(x_dev, static_cast<_Float16*>(at_dev), (int)rows, (int)k, (int)ld,
+                                              ns_of(prec), static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "tile_activations launch");
+  return WQ4_OK;
+}
+
+wq4_status wq4_linear_forward_tiled(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
+                                    const float* residual_dev, float* y_dev, int64_t rows, unsigned flags,
+                                    wq4_precision prec, void* stream) {
+  if (!w || !at_dev || !y_dev) return fail(WQ4_EINVAL, "null argument");
+  wq4_status s = check_prec(prec);
+  if (s != WQ4_OK) return s;
+  if ((flags & WQ4_EPI_RESIDUAL) && !residual_dev) return fail(WQ4_EINVAL, "WQ4_EPI_RESIDUAL without residual");
+  if (rows < 0 || rows > (1 << 24)) return fail(WQ4_ESHAPE, "bad row count");
+  if (rows == 0) return WQ4_OK;
+  DeviceGuard dg(w->device);
+  wq4::EpiArgs epi = make_epi(bias_dev, (flags & WQ4_EPI_RESIDUAL) ? residual_dev : nullptr, y_dev, (int)w->g.n,
+                              (int)rows, (int)w->g.n, (flags & WQ4_EPI_GELU) != 0);
+  hipError_t e = wq4::launch_q4_gemm(w->g, w->nib, w->sc, static_cast<const _Float16*>(at_dev), (int)rows, epi,
+                                     wq4::kEpiF32, ns_of(prec), use_decode(rows), static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "q4_gemm launch");
+  return WQ4_OK;
+}
+
+wq4_status wq4_linear_forward_tiled_out(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
+                                        void* at_out_dev, size_t at_out_bytes, int64_t rows, unsigned flags,
+                                        wq4_precision prec, void* stream) {
+  if (!w || !at_dev || !at_out_dev) return fail(WQ4_EINVAL, "null argument");
+  wq4_status s = check_prec(prec);
+  if (s != WQ4_OK) return s;
+  if (flags & WQ4_EPI_RESIDUAL) return fail(WQ4_EUNSUPPORTED, "residual with a tiled output");
+  if (rows < 0 || rows > (1 << 24)) return fail(WQ4_ESHAPE, "bad row count");
+  if (w->g.n % 32 != 0) return fail(WQ4_ESHAPE, "tiled output needs N % 32 == 0");
+  if (at_out_bytes < wq4::atiled_bytes(rows, w->g.n, ns_of(prec)))
+    return fail(WQ4_ENOMEM, "A-tiled output buffer too small");
+  if (rows == 0) return WQ4_OK;
+  DeviceGuard dg(w->device);
+  wq4::EpiArgs epi = make_epi(bias_dev, nullptr, nullptr, (int)w->g.n, (int)rows, (int)w->g.n,
+                              (flags & WQ4_EPI_GELU) != 0);
+  epi.out_tiled = static_cast<_Float16*>(at_out_dev);
+  epi.nbp_next = (int)((w->g.n / 32 + 1) / 2);
+  hipError_t e = wq4::launch_q4_gemm(w->g, w->nib, w->sc, static_cast<const _Float16*>(at_dev), (int)rows, epi,
+                                     wq4::kEpiTiled, ns_of(prec), use_decode(rows), static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "q4_gemm launch");
+  return WQ4_OK;
+}
+
+static wq4_status check_nk(int64_t n, int64_t k) {
+  if (n <= 0 || k <= 0 || k % 32 != 0 || n > (1 << 24) || k > (1 << 24))
+    return fail(WQ4_ESHAPE, "bad Q4_0 shape [" + std::to_string(n) + ", " + std::to_string(k) + "]");
+  return WQ4_OK;
+}
+
+wq4_status wq4_debug_repacked_bytes(int64_t n, int64_t k, size_t* nib_bytes, size_t* sc_bytes) {
+  wq4_status s = check_nk(n, k);
+  if (s != WQ4_OK) return s;
+  if (!nib_bytes || !sc_bytes) return fail(WQ4_EINVAL, "null argument");
+  const wq4::Q4Geom g = wq4::make_geom(n, k);
+  *nib_bytes = g.nib_bytes();
+  *sc_bytes = g.sc_bytes();
+  return WQ4_OK;
+}
+
+wq4_status wq4_debug_repack(const uint8_t* raw, int64_t n, int64_t k, uint8_t* nib_out, uint32_t* sc_out) {
+  wq4_status s = check_nk(n, k);
+  if (s != WQ4_OK) return s;
+  if (!raw || !nib_out || !sc_out) return fail(WQ4_EINVAL, "null argument");
+  wq4::repack_q4(raw, wq4::make_geom(n, k), nib_out, sc_out);
+  return WQ4_OK;
+}
+
+wq4_status wq4_debug_unrepack(const uint8_t* nib, const uint32_t* sc, int64_t n, int64_t k, uint8_t* raw_out) {
+  wq4_status s = check_nk(n, k);
+  if (s != WQ4_OK) return s;
+  if (!nib || !sc || !raw_out) return fail(WQ4_EINVAL, "null argument");
+  wq4::unrepack_q4(nib, sc, wq4::make_geom(n, k), raw_out);
+  return WQ4_OK;
+}
+
+// Q4FFN::forward, src/model/layers.rs:54-58.
+wq4_status wq4_ffn_forward(const wq4_tensor* fc1, const float* b1_dev, const wq4_tensor* fc2,
+                           const float* b2_dev, const float* x_dev, float* y_dev, int64_t b, int64_t m,
+                           void* stream) {
+  if (!fc1 || !fc2) return fail(WQ4_EINVAL, "weights are null");
+  if (b < 0 || m < 0) return fail(WQ4_ESHAPE, "negative B or M");
+  const int64_t rows = b * m;
+  const wq4_precision prec = wq4_get_precision();
+  const int ns = ns_of(prec);
+  const size_t need = wq4::atiled_bytes(rows, fc1->g.k, ns) + wq4::atiled_bytes(rows, fc2->g.k, ns);
+  void* ws = nullptr;
+  {
+    DeviceGuard dg(fc1->device);
+    wq4_status s = arena_get(fc1->device, stream, need, &ws);
+    if (s != WQ4_OK) return s;
+  }
+  return ffn_impl(fc1, b1_dev, fc2, b2_dev, x_dev, nullptr, y_dev, rows, 0u, prec, ws, need, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,84 @@
+// wq4_device.hpp -- CDNA4 (gfx950) device helpers for the Q4_0 GEMM path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "wq4_epi.hpp"
+
+namespace wq4 {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+
+
+// tanh-approximate GELU, src/model/layers.rs:35-41.
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float s = 0.7978845608028654f;  // sqrt(2/pi)
+  float x3 = x * x * x;
+  float inner = (x + x3 * 0.044715f) * s;
+  return x * 0.5f * (tanhf(inner) + 1.0f);
+}
+
+__device__ __forceinline__ float epi_value(float acc, int row, int col, const EpiArgs& e) {
+  float v = acc;
+  if (e.bias) v = v + e.bias[col];
+  if (e.gelu) v = gelu_tanh(v);
+  if (e.residual) v = e.residual[(size_t)row * e.ldo + col] + v;
+  return v;
+}
+
+// One repacked u32 (8 nibbles, see wq4_layout.hpp) -> MFMA B operand of 8
+// exact f16 values (q - 8), element order j = 0..7.
+//   (w & 0x000F000F) | 0x64006400 = f16 pair (1024 + q_a, 1024 + q_b)
+//   (w & 0x00F000F0) | 0x64006400 = f16 pair (1024 + 16 q_a, ...)
+// then -1032 resp. *(1/16) - 72; every step is exact in f16.
+__device__ __forceinline__ half8 deq8(uint32_t w) {
+  const uint32_t C = 0x64006400u;
+  const uint32_t w8 = w >> 8;
+  const uint32_t p0 = (w & 0x000F000Fu) | C;
+  const uint32_t p1 = (w & 0x00F000F0u) | C;
+  const uint32_t p2 = (w8 & 0x000F000Fu) | C;
+  const uint32_t p3 = (w8 & 0x00F000F0u) | C;
+  const half2v off1 = {(_Float16)1032.0f, (_Float16)1032.0f};
+  const half2v inv16 = {(_Float16)0.0625f, (_Float16)0.0625f};
+  const half2v off16 = {(_Float16)72.0f, (_Float16)72.0f};
+  half2v h0 = __builtin_bit_cast(half2v, p0) - off1;
+  half2v h1 = __builtin_bit_cast(half2v, p1) * inv16 - off16;
+  half2v h2 = __builtin_bit_cast(half2v, p2) - off1;
+  half2v h3 = __builtin_bit_cast(half2v, p3) * inv16 - off16;
+  half8 r;
+  r[0] = h0[0]; r[1] = h0[1];
+  r[2] = h1[0]; r[3] = h1[1];
+  r[4] = h2[0]; r[5] = h2[1];
+  r[6] = h3[0]; r[7] = h3[1];
+  return r;
+}
+
+__device__ __forceinline__ float f16bits_to_f32(uint32_t bits16) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)bits16);
+}
+
+__device__ __forceinline__ floatx16 mfma32(const half8& a, const half8& b, const floatx16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// f32 -> (hi, lo) f16 split; hi = RNE(x), lo = RNE(x - hi).  x - hi is exact.
+__device__ __forceinline__ void split_f16(float x, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (float)hi);
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming
+// §5 T1): blocks L, L+8, L+16, ... (one XCD under round-robin dispatch) get
+// consecutive logical ids, so neighbouring tiles share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int L, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = L % 8, idx = L / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace wq4
