@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Benchmark: Whisper Large-V3 Q4_0 real-time factor on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One "step" = one batch of synthetic 30-s clips transcribed end to end on each
+GPU: conv front-end + 32-layer encoder + cross-K/V + prompt + greedy KV-cached
+decode (whisper.rs:51-128), mel already resident in HBM, token ids back on the
+host.  Workload at N = 1: BASELINE.json config 4's per-GPU shard (32 clips of
+the 256-clip / 8-GPU job); each rank runs its own clips (weak scaling, no
+collective on the data path -- one process per GPU, independent replicas).
+value = audio seconds of all ranks' clips / max-over-ranks wall seconds.
+
+roofline: the Q4 GEMMs (the north-star kernel, MFMA tile kernel), timed live
+with HIP events on their launch stream during the timed steps; algorithmic
+FLOPs = 2*M*N*K per launch.  cpu_baseline: the reference's CPU dequant->GEMM
+path (src/gguf/tests.rs:60-87,172-184, restated in oracle/q4_oracle.c), one
+core, on one Large-V3 encoder layer's Q4 GEMMs at --cpu-rows rows, scaled to
+a clip's Q4 GEMM FLOPs (a lower bound on the CPU's per-clip time).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "whisper-burn_amd"))
+
+METRIC = "real-time factor (audio-s/wall-s) Whisper Large-V3 Q4 @1/2/4/8 MI355X"
+CLIP_SECONDS = 30.0
+PEAK_MFMA_TFLOPS = 2500.0  # dense f16/bf16, MI355X_MICROARCH.md:43
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md:36
+
+
+def clip_q4_gflop(cfg: dict, tokens: float) -> float:
+    """Algorithmic Q4 GEMM GFLOP per clip."""
+    D, T = cfg["n_audio_state"], cfg["n_audio_ctx"]
+    Dt = cfg["n_text_state"]
+    enc = cfg["n_audio_layer"] * 2 * T * (4 * D * D + 2 * 4 * D * D)
+    cross = cfg["n_text_layer"] * 2 * T * 2 * Dt * D
+    per_tok = cfg["n_text_layer"] * 2 * (6 * Dt * Dt + 2 * 4 * Dt * Dt)
+    return (enc + cross + per_tok * (4 + tokens)) * 1e-9
+
+
+def cpu_baseline(cfg: dict, rows: int, tokens: float) -> dict:
+    """Reference CPU dequant -> naive GEMM on one encoder layer's Q4 GEMMs."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+
+    import oracle
+
+    D = cfg["n_audio_state"]
+    shapes = [(D, D)] * 4 + [(4 * D, D), (D, 4 * D)]  # q, k, v, out, fc1, fc2
+    rng = np.random.default_rng(0)
+    t = 0.0
+    flops = 0.0
+    for n, k in shapes:
+        q = oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.02).astype(np.float32))
+        x = rng.standard_normal(rows * k).astype(np.float32)
+        t0 = time.perf_counter()
+        oracle.cpu_dequant_gemm(q, x, rows, k, n)
+        t += time.perf_counter() - t0
+        flops += 2.0 * rows * n * k
+    sec_per_clip = t * (clip_q4_gflop(cfg, tokens) * 1e9 / flops)
+    return {"value": CLIP_SECONDS / sec_per_clip, "unit": "audio-s/wall-s", "cores": 1, "kind": "port",
+            "sample": f"one Large-V3 encoder layer's 6 Q4 GEMMs at {rows} rows ({flops * 1e-9:.1f} GFLOP, "
+                      f"{t:.1f} s, {flops / t * 1e-9:.2f} GFLOP/s), scaled to {clip_q4_gflop(cfg, tokens):.0f} "
+                      f"GFLOP of Q4 GEMMs per clip (lower bound on CPU time)"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--variant", default="large_v3", choices=["large_v3", "medium", "tiny_test"])
+    ap.add_argument("--clips-per-gpu", type=int, default=32)
+    ap.add_argument("--max-tokens", type=int, default=224)
+    ap.add_argument("--lang", type=int, default=50259, help="language token; -1 = auto-detect")
+    ap.add_argument("--precision", default="f16x2", choices=["f16x2", "f16"])
+    ap.add_argument("--fixed-length", action="store_true", help="ignore EOT (always max-tokens steps)")
+    ap.add_argument("--cpu-rows", type=int, default=750)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--json-out", default=None)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+
+    import whisper_amd
+    import wq4
+
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    prec = wq4.PREC_F16X2 if args.precision == "f16x2" else wq4.PREC_F16
+    t_load = time.perf_counter()
+    model = whisper_amd.WhisperModel(args.variant, args.seed, max_batch=args.clips_per_gpu, device=local_rank,
+                                     precision=prec)
+    t_load = time.perf_counter() - t_load
+    cfg = model.config
+    B = args.clips_per_gpu
+    n_mels = cfg["n_mels"]
+
+    def batch(s: int):
+        base = 0x5EED0000 + (rank * (args.warmup + args.steps) + s) * B
+        arr = np.stack([whisper_amd.synth_uniform(base + i, "mel", n_mels * 3000, -1.5, 1.0) for i in range(B)])
+        return torch.from_numpy(arr.reshape(B, n_mels, 3000)).to(f"cuda:{local_rank}")
+
+    mels = [batch(s) for s in range(args.warmup + args.steps)]  # resident in HBM before timing
+    lang = None if args.lang < 0 else args.lang
+    for s in range(args.warmup):
+        model.transcribe(mels[s], lang, args.max_tokens, eot_stop=not args.fixed_length)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    model.profile_read(reset=True)
+    model.profile_enable(True)
+    ntok = []
+    timings = []
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        toks = model.transcribe(mels[args.warmup + s], lang, args.max_tokens, eot_stop=not args.fixed_length)
+        ntok += [len(t) for t in toks]
+        timings.append(model.last_timings())
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    model.profile_enable(False)
+    prof = model.profile_read(reset=True)
+    if dist:
+        tt = torch.tensor([elapsed], device=f"cuda:{local_rank}", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    clips = world * B * args.steps
+    value = clips * CLIP_SECONDS / elapsed
+
+    if rank == 0:
+        q4 = prof["q4_gemm"]
+        achieved = q4["gflop"] / (q4["ms"] * 1e-3) * 1e-3 if q4["ms"] > 0 else 0.0
+        mean_tok = float(np.mean(ntok)) if ntok else 0.0
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "audio-s/wall-s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp16x2" if prec == wq4.PREC_F16X2 else "fp16", "data": "synthetic",
+            "config": {"workload": f"Whisper {args.variant} Q4_0, {B} synthetic 30-s clips per GPU per step "
+                                   f"(BASELINE config 4 shard), greedy KV-cached decode, max {args.max_tokens} "
+                                   f"tokens, {'fixed length' if args.fixed_length else 'EOT stop'}",
+                       "model": f"whisper-{args.variant.replace('_', '-')}-q4_0 (synthetic weights)",
+                       "global_batch": clips // args.steps, "seq_len": cfg["n_audio_ctx"],
+                       "parallelism": f"replicas{world} (independent clips, no collectives)"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_MFMA_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_MFMA_TFLOPS, 4), "traffic": None,
+                         "kernel": "q4_gemm_prefill_kernel (encoder + cross-K/V Q4 GEMMs)",
+                         "launches": q4["launches"], "avg_us": round(q4["ms"] / max(1, q4["launches"]) * 1e3, 2)},
+            "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                            "tflops": round(v["gflop"] / (v["ms"] * 1e-3) * 1e-3, 2) if v["ms"] else None,
+                            "gbs": round(v["gb"] / (v["ms"] * 1e-3), 1) if v["ms"] else None}
+                        for k, v in prof.items()},
+            "tokens_per_clip": round(mean_tok, 2),
+            "phase_ms": {k: round(float(np.mean([t[k] for t in timings])), 3)
+                         for k in ("encoder_ms", "cross_kv_ms", "prompt_ms", "decode_ms")},
+            "decode_steps": [t["steps"] for t in timings],
+            "model_load_s": round(t_load, 2),
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(model.config, args.cpu_rows, mean_tok)
+        else:
+            line["cpu_baseline"] = None
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(s + "\n")
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -143,6 +143,21 @@ wq4_status wq4_linear_forward_tiled_out(const wq4_tensor* w, const float* bias_d
                                         void* at_out_dev, size_t at_out_bytes, int64_t rows, unsigned flags,
                                         wq4_precision prec, void* stream);
 
+/* Extended operand-layout GEMM used by the model runtime: explicit kernel
+ * (0 = automatic by rows, 1 = MFMA tile "prefill", 2 = K-split "decode"),
+ * output f32 row-major y_dev, or, with WQ4_EPI_TILED_OUT, the A-tiled
+ * operand at_out_dev of a following GEMM (K' = N; N % 32 == 0).           */
+#define WQ4_EPI_TILED_OUT 4u
+wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void* at_dev, const float* residual_dev,
+                          float* y_dev, void* at_out_dev, int64_t rows, unsigned flags, wq4_precision prec,
+                          int kernel, void* stream);
+
+/* ---- conversion (scripts/convert_whisper.py:33-74) -------------------- */
+/* Q4_0-quantize n f32 values (n % 32 == 0) exactly as the reference's
+ * converter does under numpy 2: d = amax/7 (f32), f16 scale, round-half-even
+ * of v/d, nibble = (q + 8) & 0xF, low nibble = elements 0..15.             */
+wq4_status wq4_quantize_q4_0(const float* x, int64_t n, uint8_t* out);
+
 /* ---- kernel selection (exposed for tests and the bench) -------------- */
 /* 0 = automatic (by rows), 1 = force the MFMA tile kernel ("prefill"),
  * 2 = force the K-split streaming kernel ("decode").  Both compute each
@@ -150,12 +165,14 @@ wq4_status wq4_linear_forward_tiled_out(const wq4_tensor* w, const float* bias_d
 wq4_status wq4_set_kernel_policy(int policy);
 
 /* ---- host-only diagnostics (no GPU needed) ---------------------------- */
-/* Sizes of the repacked nibble / scale arrays for a [N, K] tensor. */
-wq4_status wq4_debug_repacked_bytes(int64_t n, int64_t k, size_t* nib_bytes, size_t* sc_bytes);
+/* Sizes of the repacked nibble / scale / column-scale arrays for [N, K]. */
+wq4_status wq4_debug_repacked_bytes(int64_t n, int64_t k, size_t* nib_bytes, size_t* sc_bytes, size_t* cs_bytes);
 /* The repack wq4_tensor_create applies on upload, run on the host. */
-wq4_status wq4_debug_repack(const uint8_t* raw, int64_t n, int64_t k, uint8_t* nib_out, uint32_t* sc_out);
+wq4_status wq4_debug_repack(const uint8_t* raw, int64_t n, int64_t k, uint8_t* nib_out, uint32_t* sc_out,
+                            float* colscale_out);
 /* Its inverse (raw GGUF bytes from the repacked arrays). */
-wq4_status wq4_debug_unrepack(const uint8_t* nib, const uint32_t* sc, int64_t n, int64_t k, uint8_t* raw_out);
+wq4_status wq4_debug_unrepack(const uint8_t* nib, const uint32_t* sc, const float* colscale, int64_t n, int64_t k,
+                              uint8_t* raw_out);
 
 #ifdef __cplusplus
 }

@@ -247,4 +247,14 @@ def synth_uniform(seed: int, name: str, n: int, lo: float, hi: float) -> np.ndar
         idx = np.arange(n, dtype=np.uint64) + key
     u = (splitmix64(idx) >> np.uint64(40)).astype(np.float32)  # exact: < 2^24
     unit = u * np.float32(1.0 / 16777216.0)  # exact
-    return (np.float32(lo) + unit * np.float32(hi - lo)).astype(np.float32)
+    lo32, hi32 = np.float32(lo), np.float32(hi)
+    span = np.float32(np.float64(hi32) - np.float64(lo32))
+    t = (unit * span).astype(np.float32)
+    return (lo32 + t).astype(np.float32)
+
+
+def lin_scale(k: int) -> np.float32:
+    """Uniform half-width of a synthetic linear weight with fan-in k."""
+    import math
+
+    return np.float32(1.5 / math.sqrt(k))

@@ -1,0 +1,291 @@
+"""numpy restatement of the reference Whisper model -- TEST INFRASTRUCTURE ONLY.
+
+The token / logit oracle for the model around the Q4 path.  Only tests/ and
+bench.py (as the checker) import it; the product never does.
+
+It restates, in float32 numpy (or float64 for error analysis):
+  Conv1D im2col + bias               src/model/layers.rs:77-132
+  gelu (tanh form)                   src/model/layers.rs:35-41
+  LayerNorm (eps 1e-5, biased var)   src/model/layers.rs:12-32
+  scaled_dot_product_attention       src/model/attention.rs:243-298
+  Q4MultiHeadAttention / CrossAttn   src/model/attention.rs:47-236
+  EncoderBlock / WhisperEncoder      src/model/encoder.rs:37-115
+  DecoderBlock / WhisperDecoder      src/model/decoder.rs:77-348
+  WhisperModel::transcribe + argmax  src/model/whisper.rs:51-138
+with every Q4 weight dequantized by the reference's rule (tests.rs:60-87) from
+bytes made by the reference's quantizer (convert_whisper.py:33-74, restated in
+oracle.quantize_convert_np and pinned by tests/golden).  The reference has no
+model-level golden tokens: parity of tokens is "unpinned" with
+respect to the reference binary and pinned to this restatement.
+
+The synthetic weights are generated exactly as the product does
+(whisper-burn_amd/csrc/whisper/wa_model.cpp build_synthetic): same names,
+same ranges, same generator (oracle.synth_uniform).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import oracle
+
+SOT, EOT = 50258, 50257
+MAX_TOKENS = 224  # whisper.rs:20
+MIN_TOKENS = 3  # whisper.rs:97
+
+CONFIGS = {  # src/model/config.rs:32-63 (+ the parity-test configuration)
+    "large_v3": dict(n_mels=128, n_audio_ctx=1500, n_audio_state=1280, n_audio_head=20, n_audio_layer=32,
+                     n_text_ctx=448, n_text_state=1280, n_text_head=20, n_text_layer=32, n_vocab=51866, n_lang=100),
+    "medium": dict(n_mels=80, n_audio_ctx=1500, n_audio_state=1024, n_audio_head=16, n_audio_layer=24,
+                   n_text_ctx=448, n_text_state=1024, n_text_head=16, n_text_layer=24, n_vocab=51865, n_lang=99),
+    "tiny_test": dict(n_mels=80, n_audio_ctx=1500, n_audio_state=384, n_audio_head=6, n_audio_layer=2,
+                      n_text_ctx=448, n_text_state=384, n_text_head=6, n_text_layer=2, n_vocab=51866, n_lang=100),
+}
+VARIANT_ID = {"large_v3": 0, "medium": 1, "tiny_test": 2}
+
+
+def synthetic_mel(clip: int, n_mels: int, seed: int = 0x5EED0000) -> np.ndarray:
+    """Per-clip synthetic log-mel in the normalised range of mel.rs:136-154."""
+    return oracle.synth_uniform(seed + clip, "mel", n_mels * 3000, -1.5, 1.0).reshape(n_mels, 3000)
+
+
+class SynthWhisper:
+    def __init__(self, variant: str = "tiny_test", seed: int = 1234, dtype=np.float32):
+        self.cfg = dict(CONFIGS[variant])
+        self.seed = seed
+        self.dt = dtype
+        self.w: dict[str, np.ndarray] = {}
+        self._build()
+
+    # ---------------------------------------------------------- weights --
+    def _u(self, name, n, lo, hi):
+        return oracle.synth_uniform(self.seed, name, n, lo, hi)
+
+    def _q4(self, name, n, k):
+        a = float(oracle.lin_scale(k))
+        q = oracle.quantize_convert_np(self._u(name, n * k, -a, a))
+        return oracle.dequantize_np(q, n * k).reshape(n, k).astype(self.dt)
+
+    def _vec(self, name, n, lo, hi):
+        return self._u(name, n, lo, hi).astype(self.dt)
+
+    def _build(self):
+        c = self.cfg
+        D, Dt = c["n_audio_state"], c["n_text_state"]
+        F, Ft = 4 * D, 4 * Dt
+        w = self.w
+        for nm, cin in (("encoder.conv1", c["n_mels"]), ("encoder.conv2", D)):
+            a = float(oracle.lin_scale(3 * cin))
+            w[nm + ".weight"] = self._u(nm + ".weight", D * cin * 3, -a, a).reshape(D, cin, 3).astype(self.dt)
+            w[nm + ".bias"] = self._vec(nm + ".bias", D, -0.02, 0.02)
+        w["encoder.positional_embedding"] = self._vec("encoder.positional_embedding", c["n_audio_ctx"] * D, -0.1,
+                                                      0.1).reshape(c["n_audio_ctx"], D)
+
+        def ln(p, d):
+            w[p + ".weight"] = self._vec(p + ".weight", d, 0.9, 1.1)
+            w[p + ".bias"] = self._vec(p + ".bias", d, -0.05, 0.05)
+
+        def lin(p, n, k, bias=True):
+            w[p + ".weight"] = self._q4(p + ".weight", n, k)
+            if bias:
+                w[p + ".bias"] = self._vec(p + ".bias", n, -0.02, 0.02)
+
+        for i in range(c["n_audio_layer"]):
+            p = f"encoder.blocks.{i}"
+            ln(p + ".attn_ln", D)
+            lin(p + ".attn.query", D, D)
+            lin(p + ".attn.key", D, D, bias=False)
+            lin(p + ".attn.value", D, D)
+            lin(p + ".attn.out", D, D)
+            ln(p + ".mlp_ln", D)
+            lin(p + ".mlp.0", F, D)
+            lin(p + ".mlp.2", D, F)
+        ln("encoder.ln_post", D)
+        a = float(oracle.lin_scale(Dt))
+        w["decoder.token_embedding.weight"] = self._u("decoder.token_embedding.weight", c["n_vocab"] * Dt, -a,
+                                                      a).reshape(c["n_vocab"], Dt).astype(self.dt)
+        w["decoder.positional_embedding"] = self._vec("decoder.positional_embedding", c["n_text_ctx"] * Dt, -0.02,
+                                                      0.02).reshape(c["n_text_ctx"], Dt)
+        for i in range(c["n_text_layer"]):
+            p = f"decoder.blocks.{i}"
+            ln(p + ".attn_ln", Dt)
+            lin(p + ".attn.query", Dt, Dt)
+            lin(p + ".attn.key", Dt, Dt, bias=False)
+            lin(p + ".attn.value", Dt, Dt)
+            lin(p + ".attn.out", Dt, Dt)
+            ln(p + ".cross_attn_ln", Dt)
+            lin(p + ".cross_attn.query", Dt, Dt)
+            lin(p + ".cross_attn.key", Dt, D, bias=False)  # loader.rs:205-210
+            lin(p + ".cross_attn.value", Dt, D)
+            lin(p + ".cross_attn.out", Dt, Dt)
+            ln(p + ".mlp_ln", Dt)
+            lin(p + ".mlp.0", Ft, Dt)
+            lin(p + ".mlp.2", Dt, Ft)
+        ln("decoder.ln", Dt)
+
+    # ----------------------------------------------------------- layers --
+    def linear(self, x, p, bias=True):  # linear.rs:34-40
+        y = x @ self.w[p + ".weight"].T
+        if bias and (p + ".bias") in self.w:
+            y = y + self.w[p + ".bias"]
+        return y.astype(self.dt)
+
+    def layer_norm(self, x, p):  # layers.rs:23-31
+        eps = self.dt(1e-5)
+        mean = x.mean(axis=-1, keepdims=True, dtype=self.dt)
+        c = x - mean
+        var = (c * c).mean(axis=-1, keepdims=True, dtype=self.dt)
+        return ((c / np.sqrt(var + eps)) * self.w[p + ".weight"] + self.w[p + ".bias"]).astype(self.dt)
+
+    def gelu(self, x):  # layers.rs:35-41
+        s = self.dt(np.sqrt(2.0 / np.pi))
+        x3 = x * x * x
+        inner = (x + x3 * self.dt(0.044715)) * s
+        return (x * self.dt(0.5) * (np.tanh(inner) + self.dt(1.0))).astype(self.dt)
+
+    def conv1d(self, x, p, stride):  # layers.rs:77-132, padding 1
+        W, b = self.w[p + ".weight"], self.w[p + ".bias"]
+        B, C, T = x.shape
+        N, _, K = W.shape
+        t_out = (T + 2 - K) // stride + 1
+        xp = np.pad(x, ((0, 0), (0, 0), (1, 1)))
+        cols = [xp[:, :, k: k + stride * (t_out - 1) + 1: stride] for k in range(K)]
+        col = np.concatenate(cols, axis=1).transpose(0, 2, 1)  # [B, T_out, K*C], k-major
+        wf = W.transpose(0, 2, 1).reshape(N, K * C)
+        out = (col @ wf.T + b).astype(self.dt)
+        return out.transpose(0, 2, 1)  # [B, N, T_out]
+
+    def sdpa(self, q, k, v, n_heads, causal):  # attention.rs:243-298
+        B, Tq, Dm = q.shape
+        Tk = k.shape[1]
+        hd = 64
+        qh = q.reshape(B, Tq, n_heads, hd).transpose(0, 2, 1, 3)
+        kh = k.reshape(B, Tk, n_heads, hd).transpose(0, 2, 1, 3)
+        vh = v.reshape(B, Tk, n_heads, hd).transpose(0, 2, 1, 3)
+        scores = (qh @ kh.transpose(0, 1, 3, 2)) / self.dt(8.0)
+        if causal and Tq > 1:
+            mask = np.triu(np.full((Tq, Tk), -np.inf, self.dt), 1)
+            scores = scores + mask
+        m = scores.max(axis=-1, keepdims=True)
+        e = np.exp(scores - m)
+        attn = e / e.sum(axis=-1, keepdims=True)
+        out = (attn @ vh).transpose(0, 2, 1, 3).reshape(B, Tq, n_heads * hd)
+        return out.astype(self.dt)
+
+    # ---------------------------------------------------------- encoder --
+    def encode(self, mel: np.ndarray) -> np.ndarray:  # encoder.rs:87-115
+        c = self.cfg
+        x = self.gelu(self.conv1d(mel.astype(self.dt), "encoder.conv1", 1))
+        x = self.gelu(self.conv1d(x, "encoder.conv2", 2))
+        x = x.transpose(0, 2, 1)
+        x = (x + self.w["encoder.positional_embedding"][: x.shape[1]]).astype(self.dt)
+        for i in range(c["n_audio_layer"]):
+            p = f"encoder.blocks.{i}"
+            r = x
+            h = self.layer_norm(x, p + ".attn_ln")
+            q = self.linear(h, p + ".attn.query")
+            k = self.linear(h, p + ".attn.key", bias=False)
+            v = self.linear(h, p + ".attn.value")
+            x = (r + self.linear(self.sdpa(q, k, v, c["n_audio_head"], False), p + ".attn.out")).astype(self.dt)
+            r = x
+            h = self.layer_norm(x, p + ".mlp_ln")
+            h = self.linear(self.gelu(self.linear(h, p + ".mlp.0")), p + ".mlp.2")
+            x = (r + h).astype(self.dt)
+        return self.layer_norm(x, "encoder.ln_post")
+
+    # ---------------------------------------------------------- decoder --
+    def init_cache(self, enc):
+        c = self.cfg
+        cache = []
+        for i in range(c["n_text_layer"]):
+            p = f"decoder.blocks.{i}.cross_attn"
+            cache.append({"k": None, "v": None, "ck": self.linear(enc, p + ".key", bias=False),
+                          "cv": self.linear(enc, p + ".value")})
+        return cache
+
+    def decoder_pass(self, tokens: np.ndarray, positions: np.ndarray, cache, fresh: bool) -> np.ndarray:
+        """fresh=True: forward_prompt / forward_init_cache (decoder.rs:251-296):
+        causal inside the tokens, self cache REPLACED.  fresh=False:
+        decode_step (decoder.rs:306-348): cache appended.  Returns logits of
+        the last position [B, V]."""
+        c = self.cfg
+        te, pe = self.w["decoder.token_embedding.weight"], self.w["decoder.positional_embedding"]
+        x = (te[tokens] + pe[positions][None, :, :]).astype(self.dt)  # [B, T, D]
+        for i in range(c["n_text_layer"]):
+            p = f"decoder.blocks.{i}"
+            L = cache[i]
+            r = x
+            h = self.layer_norm(x, p + ".attn_ln")
+            q = self.linear(h, p + ".attn.query")
+            k = self.linear(h, p + ".attn.key", bias=False)
+            v = self.linear(h, p + ".attn.value")
+            if fresh or L["k"] is None:
+                L["k"], L["v"] = k, v
+            else:
+                L["k"] = np.concatenate([L["k"], k], axis=1)
+                L["v"] = np.concatenate([L["v"], v], axis=1)
+            a = self.sdpa(q, L["k"], L["v"], c["n_text_head"], causal=fresh)
+            x = (r + self.linear(a, p + ".attn.out")).astype(self.dt)
+            r = x
+            h = self.layer_norm(x, p + ".cross_attn_ln")
+            q = self.linear(h, p + ".cross_attn.query")
+            a = self.sdpa(q, L["ck"], L["cv"], c["n_text_head"], causal=False)
+            x = (r + self.linear(a, p + ".cross_attn.out")).astype(self.dt)
+            r = x
+            h = self.layer_norm(x, p + ".mlp_ln")
+            x = (r + self.linear(self.gelu(self.linear(h, p + ".mlp.0")), p + ".mlp.2")).astype(self.dt)
+        x = self.layer_norm(x, "decoder.ln")
+        return (x[:, -1, :] @ te.T).astype(self.dt)
+
+    # ----------------------------------------------------------- driver --
+    @staticmethod
+    def argmax_last(v: np.ndarray) -> int:
+        """Rust Iterator::max_by keeps the LAST of equal maxima (whisper.rs:131-138)."""
+        return int(len(v) - 1 - np.argmax(v[::-1]))
+
+    def transcribe(self, mel: np.ndarray, lang_token: int | None = 50259, max_tokens: int = MAX_TOKENS,
+                   eot_stop: bool = True, return_logits: bool = False):
+        """WhisperModel::transcribe (whisper.rs:51-128), batched over clips."""
+        c = self.cfg
+        B = mel.shape[0]
+        enc = self.encode(mel)
+        cache = self.init_cache(enc)
+        transcribe_tok = 50260 + c["n_lang"]
+        notime = transcribe_tok + 4
+        if lang_token is not None:
+            prompt = np.array([[SOT, lang_token, transcribe_tok, notime]] * B)
+            logits = self.decoder_pass(prompt, np.arange(4), cache, fresh=True)
+            position = 4
+        else:
+            logits = self.decoder_pass(np.full((B, 1), SOT), np.arange(1), cache, fresh=True)
+            lo, hi = 50259, 50259 + c["n_lang"]
+            langs = [lo + self.argmax_last(logits[b, lo:hi]) for b in range(B)]
+            prompt = np.array([[lg, transcribe_tok, notime] for lg in langs])
+            logits = self.decoder_pass(prompt, np.arange(3), cache, fresh=True)  # cache overwritten
+            position = 1 + 3  # whisper.rs:74,93
+        first_logits = logits.copy()
+        logits = logits.copy()
+        logits[:, EOT] = -np.inf
+        nxt = [self.argmax_last(logits[b]) for b in range(B)]
+        out = [[] for _ in range(B)]
+        done = [False] * B
+        step_logits = []
+        for step in range(max_tokens):
+            for b in range(B):
+                if not done[b]:
+                    if eot_stop and nxt[b] == EOT:
+                        done[b] = True
+                    else:
+                        out[b].append(nxt[b])
+            if all(done):
+                break
+            logits = self.decoder_pass(np.array(nxt)[:, None], np.array([position]), cache, fresh=False)
+            if return_logits:
+                step_logits.append(logits.copy())
+            position += 1
+            if step + 1 < MIN_TOKENS:
+                logits = logits.copy()
+                logits[:, EOT] = -np.inf
+            nxt = [self.argmax_last(logits[b]) for b in range(B)]
+        if return_logits:
+            return out, first_logits, step_logits
+        return out

@@ -39,9 +39,10 @@ def test_no_oracle_symbols_in_product():
 def test_repack_roundtrip_lossless(n, k):
     rng = np.random.default_rng(n * 7 + k)
     raw = rng.integers(0, 256, n * k // 32 * 18, dtype=np.uint8)
-    nib, sc = wq4.debug_repack(raw, n, k)
+    raw.reshape(-1, 18)[:, 1] &= 0x3F  # finite f16 scales of mixed magnitude (NaN/inf rows are tested below)
+    nib, sc, cs = wq4.debug_repack(raw, n, k)
     assert nib.size == ((n + 63) // 64 * 2) * ((k // 32 + 1) // 2) * 1024
-    back = wq4.debug_unrepack(nib, sc, n, k)
+    back = wq4.debug_unrepack(nib, sc, cs, n, k)
     assert np.array_equal(back, raw)
     # same information content: 4.5 bits per weight + padding only
     assert nib.size + sc.size * 4 >= raw.size
@@ -53,7 +54,7 @@ def test_repack_layout_spec():
     n, k = 64, 128
     w = oracle.closed_form(1, n * k)
     raw = oracle.quantize_convert_np(w)
-    nib, sc = wq4.debug_repack(raw, n, k)
+    nib, sc, cs = wq4.debug_repack(raw, n, k)
     nbp = 2
     words = nib.view(np.uint32).reshape(2, nbp, 64, 4)
     blocks = raw.reshape(n, k // 32, 18)
@@ -68,8 +69,30 @@ def test_repack_layout_spec():
                         q = [(b >> 4) if kk else (b & 15) for b in by]
                         want = sum(int(q[2 * i]) << (4 * i) | int(q[2 * i + 1]) << (16 + 4 * i) for i in range(4))
                         assert words[nt, bp, lane, bi * 2 + kk] == want
-                    d = int(blk[0]) | int(blk[1]) << 8
-                    assert (int(sc.reshape(2, nbp, 32)[nt, bp, r]) >> (16 * bi)) & 0xFFFF == d
+                    d = np.array([int(blk[0]) | int(blk[1]) << 8], np.uint16).view(np.float16)[0]
+                    ds = np.array([(int(sc.reshape(2, nbp, 32)[nt, bp, r]) >> (16 * bi)) & 0xFFFF],
+                                  np.uint16).view(np.float16)[0]
+                    # d' = d * 2^s exactly, colscale = 2^-s, 8 * max d' <= 2^15
+                    assert float(ds) * float(cs[32 * nt + r]) == float(d)
+                    assert abs(float(ds)) <= 4096.0
+
+
+def test_repack_extreme_scales_lossless():
+    """Rows whose scales span > 2^26 (or hold inf/NaN/subnormal) keep s = 0."""
+    n, k = 64, 256
+    rng = np.random.default_rng(4)
+    raw = rng.integers(0, 256, n * k // 32 * 18, dtype=np.uint8).reshape(n, k // 32, 18)
+    def put(row, blk, val):
+        raw[row, blk, :2] = np.array([val], np.float16).view(np.uint8)
+    put(0, 0, 60000.0); put(0, 1, 6e-8)          # ratio 1e12
+    put(1, 0, np.inf); put(2, 3, np.nan); put(3, 2, 0.0)
+    for b in range(8):
+        put(4, b, 3e-7)                            # all-subnormal row
+    raw = raw.ravel()
+    nib, sc, cs = wq4.debug_repack(raw, n, k)
+    assert cs[0] == 1.0 and cs[1] == 1.0 and cs[2] == 1.0
+    assert cs[4] < 1.0  # subnormal scales are shifted up into the normal range
+    assert np.array_equal(wq4.debug_unrepack(nib, sc, cs, n, k), raw)
 
 
 def test_deq8_arithmetic_is_exact():
@@ -101,12 +124,6 @@ def test_create_rejects_bad_byte_count():
     raw = np.zeros(17, np.uint8)
     st, msg = _create(raw, 1, 32)
     assert st == 3 and "expected 18 for 1 blocks, got 17" in msg
-
-
-def test_create_rejects_partial_block_rows():
-    raw = np.zeros(18, np.uint8)
-    st, msg = _create(raw, 2, 16)  # 32 elements but K % 32 != 0
-    assert st == 2 and "K % 32" in msg
 
 
 def test_precision_and_policy_setters():

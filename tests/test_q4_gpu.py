@@ -275,6 +275,17 @@ def test_activation_range_edges(torch):
         assert_q4_close(y.reshape(m, n), x.reshape(m, k), deq, what=f"scale {scale}")
 
 
+def test_partial_block_rows_dequantize_but_refuse_matmul(torch):
+    """[16, 16]: accepted like the reference (only N*K % 32 is checked,
+    tensor.rs:38-42); the GEMM needs whole blocks per row (shader.wgsl:69)."""
+    x = oracle.closed_form(4, 256)
+    q = oracle.quantize_test(x)
+    t = wq4.Q4Tensor.from_q4_bytes(q, [16, 16])
+    assert np.array_equal(t.raw_bytes(), q)
+    with pytest.raises(wq4.WQ4Error, match="K % 32"):
+        wq4.q4_matmul(torch.zeros((1, 1, 16), dtype=torch.float32, device="cuda:0"), t)
+
+
 def test_zero_rows_is_noop(torch):
     q, _ = make_weights(64, 128)
     t = wq4.Q4Tensor.from_q4_bytes(q, [64, 128])

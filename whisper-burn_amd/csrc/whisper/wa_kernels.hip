@@ -1,0 +1,675 @@
+// wa_kernels.hip -- gfx950 kernels of the Whisper model around the Q4 path.
+//
+// Reference semantics (zerr0o/whisper-burn):
+//   LayerNorm        src/model/layers.rs:12-32   (eps 1e-5, biased variance)
+//   GELU (tanh)      src/model/layers.rs:35-41
+//   Conv1D + GELU    src/model/layers.rs:62-132, encoder.rs:87-106
+//   SDPA             src/model/attention.rs:243-298 (scores / sqrt(64),
+//                    causal mask only when q_len > 1, softmax over keys)
+//   KV-cached decode src/model/attention.rs:93-125, decoder.rs:77-112
+//   logits / argmax  src/model/decoder.rs:289-292, 342-347; whisper.rs:131-138
+// Every product here is f32 x f32 (v_mfma_f32_32x32x2_f32: exact products,
+// f32 accumulation) or f32 VALU; only the operands handed to the Q4 GEMMs
+// are written in the f16 hi/lo A-tiled layout (wq4_layout.hpp).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "../wq4_device.hpp"
+#include "wa_kernels.hpp"
+
+namespace wa {
+
+using wq4::floatx16;
+using wq4::floatx4;
+using wq4::half8;
+
+constexpr int kEOT = 50257;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ floatx16 mfma_f32(float a, float b, const floatx16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// Index (in halves) of element (row, k) of an A-tiled operand with kbp
+// (even) Q4 blocks per row, split s.
+__device__ __forceinline__ size_t atile_index(int row, int k, int kbp, int ns, int s) {
+  const int mt = row >> 5, r = row & 31;
+  const int b = k >> 5, kk = (k >> 4) & 1, hh = (k >> 3) & 1, j = k & 7;
+  return (((((size_t)mt * kbp + b) * 2 + kk) * ns + s) * 64 + (r + 32 * hh)) * 8 + j;
+}
+
+// Write 4 consecutive k (k % 4 == 0) of one row into the A-tiled operand.
+template <int NS>
+__device__ __forceinline__ void atile_store4(_Float16* t, int row, int k, int kbp, float a, float b, float c,
+                                             float d) {
+  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+  half4 hi, lo;
+  const float v[4] = {a, b, c, d};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    _Float16 x, y;
+    wq4::split_f16(v[j], x, y);
+    hi[j] = x;
+    lo[j] = y;
+  }
+  *reinterpret_cast<half4*>(t + atile_index(row, k, kbp, NS, 0)) = hi;
+  if constexpr (NS == 2) *reinterpret_cast<half4*>(t + atile_index(row, k, kbp, NS, 1)) = lo;
+}
+
+__host__ __device__ inline int kbp_of(int k) { return ((k / 32 + 1) / 2) * 2; }
+
+// ------------------------------------------------------------------ LN --
+template <int NS, bool TILED>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                        const float* __restrict__ bb, int M, int D,
+                                                        _Float16* __restrict__ tiled, float* __restrict__ out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int kbp = kbp_of(D);
+  const int rows_total = TILED ? ((M + 31) / 32) * 32 : M;
+  for (int rr = 0; rr < 8; ++rr) {
+    const int row = blockIdx.x * 32 + wave * 8 + rr;
+    if (row >= rows_total) break;
+    if (row < M) {
+      const float* xr = x + (size_t)row * D;
+      float s = 0.0f;
+      for (int k = lane * 4; k < D; k += 256) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(xr + k);
+        s += (v[0] + v[1]) + (v[2] + v[3]);
+      }
+      const float mean = wave_sum(s) / (float)D;
+      float s2 = 0.0f;
+      for (int k = lane * 4; k < D; k += 256) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(xr + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float c = v[j] - mean;
+          s2 += c * c;
+        }
+      }
+      const float den = sqrtf(wave_sum(s2) / (float)D + 1e-5f);
+      for (int k = lane * 4; k < D; k += 256) {
+        const floatx4 v = *reinterpret_cast<const floatx4*>(xr + k);
+        const floatx4 g = *reinterpret_cast<const floatx4*>(w + k);
+        const floatx4 be = *reinterpret_cast<const floatx4*>(bb + k);
+        float y[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[j] = ((v[j] - mean) / den) * g[j] + be[j];
+        if constexpr (TILED)
+          atile_store4<NS>(tiled, row, k, kbp, y[0], y[1], y[2], y[3]);
+        else
+          *reinterpret_cast<floatx4*>(out + (size_t)row * D + k) = floatx4{y[0], y[1], y[2], y[3]};
+      }
+    } else if constexpr (TILED) {
+      for (int k = lane * 4; k < D; k += 256) atile_store4<NS>(tiled, row, k, kbp, 0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+hipError_t launch_layernorm(const float* x, const float* w, const float* b, int M, int D, _Float16* tiled, int ns,
+                            float* out, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  const dim3 grid((M + 31) / 32), block(256);
+  if (tiled) {
+    if (ns == 2)
+      hipLaunchKernelGGL((layernorm_kernel<2, true>), grid, block, 0, st, x, w, b, M, D, tiled, out);
+    else
+      hipLaunchKernelGGL((layernorm_kernel<1, true>), grid, block, 0, st, x, w, b, M, D, tiled, out);
+  } else {
+    hipLaunchKernelGGL((layernorm_kernel<2, false>), grid, block, 0, st, x, w, b, M, D, tiled, out);
+  }
+  return hipGetLastError();
+}
+
+// ------------------------------------------------- encoder attention --
+// One workgroup = 4 waves = 128 queries of one (clip, head); each wave owns
+// 32 queries and sweeps all keys in 32-key tiles staged in LDS.  Both
+// products are computed transposed (S^T = K Q^T, O^T = V^T P^T) so that a
+// lane owns one query: the online-softmax statistics are lane-local (plus
+// one swap with lane ^ 32).  Scores use q / 8 (exact power-of-two scaling of
+// attention.rs:266-267's division).
+template <int NS>
+__global__ __launch_bounds__(256) void encoder_attention_kernel(const float* __restrict__ qkv, int T, int H,
+                                                                _Float16* __restrict__ tiled) {
+  __shared__ float ks[32 * 65];
+  __shared__ float vs[32 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ql = lane & 31, h = lane >> 5;
+  const int head = blockIdx.y, b = blockIdx.z;
+  const int D = H * 64, ld = 3 * D;
+  const float* base = qkv + (size_t)b * T * ld;
+  const int q = blockIdx.x * 128 + wave * 32 + ql;
+
+  float qv[32];
+#pragma unroll
+  for (int s = 0; s < 32; ++s) qv[s] = q < T ? base[(size_t)q * ld + head * 64 + 2 * s + h] * 0.125f : 0.0f;
+
+  float m = -INFINITY, l = 0.0f;
+  floatx16 o0, o1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    o0[i] = 0.0f;
+    o1[i] = 0.0f;
+  }
+  const int ntile = (T + 31) / 32;
+  for (int kt = 0; kt < ntile; ++kt) {
+    const int key0 = kt * 32;
+    {
+      const int key = tid >> 3, d0 = (tid & 7) * 8;
+      const bool ok = key0 + key < T;
+      const float* kr = base + (size_t)(key0 + key) * ld + D + head * 64 + d0;
+#pragma unroll
+      for (int j = 0; j < 8; j += 4) {
+        floatx4 kv4 = ok ? *reinterpret_cast<const floatx4*>(kr + j) : floatx4{0.f, 0.f, 0.f, 0.f};
+        floatx4 vv4 = ok ? *reinterpret_cast<const floatx4*>(kr + D + j) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ks[key * 65 + d0 + j + e] = kv4[e];
+          vs[key * 64 + d0 + j + e] = vv4[e];
+        }
+      }
+    }
+    __syncthreads();
+    floatx16 s;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[i] = 0.0f;
+#pragma unroll
+    for (int st = 0; st < 32; ++st) s = mfma_f32(ks[ql * 65 + 2 * st + h], qv[st], s);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (key >= T) s[i] = -INFINITY;
+      mx = fmaxf(mx, s[i]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = expf(m - mn);
+    float rs = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      s[i] = expf(s[i] - mn);
+      rs += s[i];
+    }
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      o0[i] *= alpha;
+      o1[i] *= alpha;
+    }
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int key = (st & 3) + 8 * (st >> 2) + 4 * h;
+      o0 = mfma_f32(vs[key * 64 + ql], s[st], o0);
+      o1 = mfma_f32(vs[key * 64 + 32 + ql], s[st], o1);
+    }
+    __syncthreads();
+  }
+  if (q < T) {
+    const int row = b * T + q;
+    const int kbp = kbp_of(D);
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * h;
+      atile_store4<NS>(tiled, row, head * 64 + d, kbp, o0[4 * g] * inv, o0[4 * g + 1] * inv, o0[4 * g + 2] * inv,
+                       o0[4 * g + 3] * inv);
+      atile_store4<NS>(tiled, row, head * 64 + 32 + d, kbp, o1[4 * g] * inv, o1[4 * g + 1] * inv,
+                       o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
+    }
+  }
+}
+
+hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Float16* tiled, int ns,
+                                    hipStream_t st) {
+  const dim3 grid((T + 127) / 128, H, B), block(256);
+  if (ns == 2)
+    hipLaunchKernelGGL((encoder_attention_kernel<2>), grid, block, 0, st, qkv, T, H, tiled);
+  else
+    hipLaunchKernelGGL((encoder_attention_kernel<1>), grid, block, 0, st, qkv, T, H, tiled);
+  return hipGetLastError();
+}
+
+// ------------------------------------------ decoder self-attention --
+// One workgroup per (head, clip); wave t handles new token t (Tq <= 4).
+// Keys: the KV cache entries 0 .. kv_len + t (causal inside the new tokens).
+constexpr int kMaxCtx = 448;
+
+template <int NS>
+__global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restrict__ qkv, float* __restrict__ ck,
+                                                            float* __restrict__ cv, int Tq, int H, int ctx,
+                                                            const DecodeState* state, int kv_len_host,
+                                                            _Float16* __restrict__ tiled) {
+  __shared__ float qs[4][64];
+  __shared__ float ps[4][kMaxCtx];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int head = blockIdx.x, b = blockIdx.y;
+  const int D = H * 64;
+  const int kv_len = state ? state->kv_len : kv_len_host;
+  // append the new keys / values (decoder.rs:77-112 via Tensor::cat)
+  for (int idx = tid; idx < Tq * 64; idx += 256) {
+    const int t = idx >> 6, d = idx & 63;
+    const float* src = qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + d;
+    const size_t dst = ((size_t)b * ctx + kv_len + t) * D + head * 64 + d;
+    ck[dst] = src[D];
+    cv[dst] = src[2 * D];
+    qs[t][d] = src[0] * 0.125f;
+  }
+  __syncthreads();
+  if (wave < Tq) {
+    const int t = wave;
+    const int nk = kv_len + t + 1;
+    const float* kb = ck + (size_t)b * ctx * D + head * 64;
+    const float* vb = cv + (size_t)b * ctx * D + head * 64;
+    float mx = -INFINITY;
+    for (int j = lane; j < nk; j += 64) {
+      const float* kr = kb + (size_t)j * D;
+      float dot = 0.0f;
+#pragma unroll
+      for (int d = 0; d < 64; d += 4) {
+        const floatx4 k4 = *reinterpret_cast<const floatx4*>(kr + d);
+        dot += qs[t][d] * k4[0] + qs[t][d + 1] * k4[1] + qs[t][d + 2] * k4[2] + qs[t][d + 3] * k4[3];
+      }
+      ps[t][j] = dot;
+      mx = fmaxf(mx, dot);
+    }
+    mx = wave_max(mx);
+    float sum = 0.0f;
+    for (int j = lane; j < nk; j += 64) {
+      const float p = expf(ps[t][j] - mx);
+      ps[t][j] = p;
+      sum += p;
+    }
+    sum = wave_sum(sum);
+    __builtin_amdgcn_wave_barrier();
+    float o = 0.0f;
+    for (int j = 0; j < nk; ++j) o += ps[t][j] * vb[(size_t)j * D + lane];
+    o = o / sum;
+    // lanes 4g..4g+3 hold d = 4g..4g+3 -> gather to lane 4g and store 4 halves
+    const float o1 = __shfl_down(o, 1, 64), o2 = __shfl_down(o, 2, 64), o3 = __shfl_down(o, 3, 64);
+    if ((lane & 3) == 0) atile_store4<NS>(tiled, b * Tq + t, head * 64 + lane, kbp_of(D), o, o1, o2, o3);
+  }
+}
+
+hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float* cache_v, int B, int Tq, int H,
+                                         int ctx, const DecodeState* state, int kv_len_host, _Float16* tiled,
+                                         int ns, hipStream_t st) {
+  if (Tq > 4 || ctx > kMaxCtx) return hipErrorInvalidValue;
+  const dim3 grid(H, B), block(256);
+  if (ns == 2)
+    hipLaunchKernelGGL((dec_self_attn_kernel<2>), grid, block, 0, st, qkv, cache_k, cache_v, Tq, H, ctx, state,
+                       kv_len_host, tiled);
+  else
+    hipLaunchKernelGGL((dec_self_attn_kernel<1>), grid, block, 0, st, qkv, cache_k, cache_v, Tq, H, ctx, state,
+                       kv_len_host, tiled);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------- cross-attention --
+// One workgroup per (head, clip): 4 waves split the T encoder keys; inside a
+// wave 16 lanes share one key (4 dims each), 4 keys per instruction, with
+// an online softmax per 16-lane group, merged across groups and waves.
+template <int NS>
+__global__ __launch_bounds__(256) void cross_attn_kernel(const float* __restrict__ q, const float* __restrict__ kv,
+                                                         int Tq, int T, int H, _Float16* __restrict__ tiled) {
+  __shared__ float wm[4][4], wl[4][4];
+  __shared__ float wo[4][4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int head = blockIdx.x, b = blockIdx.y;
+  const int D = H * 64;
+  const int sub = lane & 15, grp = lane >> 4;
+  floatx4 qv[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(q + (size_t)(b * Tq + t) * D + head * 64 + sub * 4)
+                   : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) qv[t] = qv[t] * 0.125f;
+  float m[4], l[4];
+  floatx4 o[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    m[t] = -INFINITY;
+    l[t] = 0.0f;
+    o[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int per_wave = (T + 3) / 4;
+  const int k0 = wave * per_wave, k1 = min(T, k0 + per_wave);
+  const float* kvb = kv + (size_t)b * T * 2 * D + head * 64 + sub * 4;
+  constexpr int U = 4;  // 16 keys per wave per iteration in flight
+  for (int j0 = k0; j0 < k1; j0 += 4 * U) {
+    floatx4 kk[U], vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + 4 * u + grp;
+      const bool ok = j < k1;
+      const float* r = kvb + (size_t)(ok ? j : k0) * 2 * D;
+      kk[u] = ok ? *reinterpret_cast<const floatx4*>(r) : floatx4{0.f, 0.f, 0.f, 0.f};
+      vv[u] = ok ? *reinterpret_cast<const floatx4*>(r + D) : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + 4 * u + grp;
+      const bool ok = j < k1;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < Tq) {
+          float dot = qv[t][0] * kk[u][0] + qv[t][1] * kk[u][1] + qv[t][2] * kk[u][2] + qv[t][3] * kk[u][3];
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1) dot += __shfl_xor(dot, off, 64);
+          if (ok) {
+            const float mn = fmaxf(m[t], dot);
+            const float alpha = expf(m[t] - mn);
+            const float p = expf(dot - mn);
+            l[t] = l[t] * alpha + p;
+            o[t] = o[t] * alpha + vv[u] * p;
+            m[t] = mn;
+          }
+        }
+      }
+    }
+  }
+  // merge the 4 groups of the wave, then the 4 waves (fixed order)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t >= Tq) break;
+#pragma unroll
+    for (int off = 16; off < 64; off <<= 1) {
+      const float m2 = __shfl_xor(m[t], off, 64), l2 = __shfl_xor(l[t], off, 64);
+      floatx4 o2;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o2[e] = __shfl_xor(o[t][e], off, 64);
+      const float mn = fmaxf(m[t], m2);
+      const float a1 = m[t] == -INFINITY ? 0.0f : expf(m[t] - mn);
+      const float a2 = m2 == -INFINITY ? 0.0f : expf(m2 - mn);
+      l[t] = l[t] * a1 + l2 * a2;
+      o[t] = o[t] * a1 + o2 * a2;
+      m[t] = mn;
+    }
+    if (grp == 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wo[wave][t][sub * 4 + e] = o[t][e];
+    }
+    if (lane == 0) {
+      wm[wave][t] = m[t];
+      wl[wave][t] = l[t];
+    }
+  }
+  __syncthreads();
+  if (wave < Tq) {
+    const int t = wave;
+    float mn = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) mn = fmaxf(mn, wm[w][t]);
+    float ls = 0.0f, os = 0.0f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float a = wm[w][t] == -INFINITY ? 0.0f : expf(wm[w][t] - mn);
+      ls += wl[w][t] * a;
+      os += wo[w][t][lane] * a;
+    }
+    const float val = os / ls;
+    const float v1 = __shfl_down(val, 1, 64), v2 = __shfl_down(val, 2, 64), v3 = __shfl_down(val, 3, 64);
+    if ((lane & 3) == 0) atile_store4<NS>(tiled, b * Tq + t, head * 64 + lane, kbp_of(D), val, v1, v2, v3);
+  }
+}
+
+hipError_t launch_cross_attention(const float* q, const float* kv, int B, int Tq, int T, int H, _Float16* tiled,
+                                  int ns, hipStream_t st) {
+  if (Tq > 4) return hipErrorInvalidValue;
+  const dim3 grid(H, B), block(256);
+  if (ns == 2)
+    hipLaunchKernelGGL((cross_attn_kernel<2>), grid, block, 0, st, q, kv, Tq, T, H, tiled);
+  else
+    hipLaunchKernelGGL((cross_attn_kernel<1>), grid, block, 0, st, q, kv, Tq, T, H, tiled);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------ conv + GELU --
+// out[b, t, n] = gelu(bias[n] + sum_{kk, c} in(b, c, t*S + kk - 1) W[n, c, kk])
+// (+ pos[t, n]).  GEMM view: rows (b, t), cols n, K = 3C (k = kk*C + c, the
+// reference's im2col order, layers.rs:92-121).  Workgroup tile 128 x 128,
+// 4 waves of 64 x 64, K chunks of 32 staged [k][m] / [k][n] in LDS.
+__global__ __launch_bounds__(256) void conv_gelu_kernel(const float* __restrict__ in, long in_bs, long in_cs,
+                                                        long in_ts, int B, int C, int T_in, int S,
+                                                        const float* __restrict__ wt, const float* __restrict__ bias,
+                                                        const float* __restrict__ pos, int N, float* __restrict__ out,
+                                                        int T_out) {
+  __shared__ float as[32][128 + 4];
+  __shared__ float bs[32][128 + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int M = B * T_out, K = 3 * C;
+  const int m0 = blockIdx.x * 128, n0 = blockIdx.y * 128;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][c][i] = 0.0f;
+
+  for (int kc = 0; kc < K; kc += 32) {
+    // stage A: 32 k x 128 m (im2col gather), B: 32 k x 128 n
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int e = it * 256 + tid;
+      const int kl = e >> 7, ml = e & 127;
+      const int k = kc + kl, m = m0 + ml;
+      float v = 0.0f;
+      if (k < K && m < M) {
+        const int kk = k / C, c = k - kk * C;
+        const int bb = m / T_out, t = m - bb * T_out;
+        const int ti = t * S + kk - 1;
+        if (ti >= 0 && ti < T_in) v = in[bb * in_bs + c * in_cs + (long)ti * in_ts];
+      }
+      as[kl][ml] = v;
+    }
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int e = it * 256 + tid;
+      const int nl = e >> 5, kl = e & 31;
+      const int k = kc + kl, n = n0 + nl;
+      bs[kl][nl] = (k < K && n < N) ? wt[(size_t)n * K + k] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int kl = 2 * s + h;
+      const float a0 = as[kl][wm + r], a1 = as[kl][wm + 32 + r];
+      const float b0 = bs[kl][wn + r], b1 = bs[kl][wn + 32 + r];
+      acc[0][0] = mfma_f32(a0, b0, acc[0][0]);
+      acc[0][1] = mfma_f32(a0, b1, acc[0][1]);
+      acc[1][0] = mfma_f32(a1, b0, acc[1][0]);
+      acc[1][1] = mfma_f32(a1, b1, acc[1][1]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = m0 + wm + 32 * a + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const int n = n0 + wn + 32 * c + r;
+        if (m < M && n < N) {
+          float v = wq4::gelu_tanh(acc[a][c][i] + bias[n]);
+          if (pos) v = v + pos[(size_t)(m % T_out) * N + n];
+          out[(size_t)m * N + n] = v;
+        }
+      }
+}
+
+hipError_t launch_conv_gelu(const float* in, long in_bs, long in_cs, long in_ts, int B, int C, int T_in,
+                            int stride, const float* w_t, const float* bias, const float* pos, int N, float* out,
+                            hipStream_t st) {
+  const int T_out = (T_in + 2 - 3) / stride + 1;
+  const dim3 grid((B * T_out + 127) / 128, (N + 127) / 128), block(256);
+  hipLaunchKernelGGL(conv_gelu_kernel, grid, block, 0, st, in, in_bs, in_cs, in_ts, B, C, T_in, stride, w_t, bias,
+                     pos, N, out, T_out);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------- embedding --
+__global__ void embed_kernel(const int* __restrict__ tokens, const float* __restrict__ te,
+                             const float* __restrict__ pe, int Tq, int D, const DecodeState* state, int pos0,
+                             float* __restrict__ x) {
+  const int row = blockIdx.x;  // b * Tq + t
+  const int t = row % Tq;
+  const int p = (state ? state->position : pos0) + t;
+  const int tok = tokens[row];
+  for (int d = threadIdx.x; d < D; d += blockDim.x)
+    x[(size_t)row * D + d] = te[(size_t)tok * D + d] + pe[(size_t)p * D + d];
+}
+
+hipError_t launch_embed(const int* tokens, const float* tok_emb, const float* pos_emb, int B, int Tq, int D,
+                        const DecodeState* state, int pos0_host, float* x, hipStream_t st) {
+  hipLaunchKernelGGL(embed_kernel, dim3(B * Tq), dim3(256), 0, st, tokens, tok_emb, pos_emb, Tq, D, state,
+                     pos0_host, x);
+  return hipGetLastError();
+}
+
+// -------------------------------------------------------------- logits --
+// logits[b, v] = sum_d h[b, d] E[v, d]; B <= 32 clips per call.  One wave =
+// 32 vocabulary rows; h staged in LDS in 256-wide k chunks.
+__global__ __launch_bounds__(256) void logits_kernel(const float* __restrict__ hid, int B, int D, long ldh,
+                                                     const float* __restrict__ emb, int V,
+                                                     float* __restrict__ logits) {
+  __shared__ float hs[32][256 + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int n = blockIdx.x * 128 + wave * 32 + r;
+  const float* er = emb + (size_t)(n < V ? n : 0) * D;
+  floatx16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+  for (int kc = 0; kc < D; kc += 256) {
+    const int kw = min(256, D - kc);
+    __syncthreads();
+    for (int e = tid; e < 32 * 256; e += 256) {
+      const int row = e >> 8, k = e & 255;
+      hs[row][k] = (row < B && k < kw) ? hid[(size_t)row * ldh + kc + k] : 0.0f;
+    }
+    __syncthreads();
+    for (int k8 = 0; k8 < kw; k8 += 8) {
+      const floatx4 e4 = n < V ? *reinterpret_cast<const floatx4*>(er + kc + k8 + 4 * h) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = mfma_f32(hs[r][k8 + 4 * h + s], e4[s], acc);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+    if (row < B && n < V) logits[(size_t)row * V + n] = acc[i];
+  }
+}
+
+hipError_t launch_logits(const float* h, int B, int D, long ldh, const float* emb, int V, float* logits,
+                         hipStream_t st) {
+  for (int b0 = 0; b0 < B; b0 += 32) {
+    const int nb = min(32, B - b0);
+    hipLaunchKernelGGL(logits_kernel, dim3((V + 127) / 128), dim3(256), 0, st, h + (size_t)b0 * ldh, nb, D, ldh,
+                       emb, V, logits + (size_t)b0 * V);
+  }
+  return hipGetLastError();
+}
+
+// -------------------------------------------------------------- argmax --
+// Rust `max_by(partial_cmp)` keeps the LAST of equal maxima (whisper.rs:131-138).
+__device__ __forceinline__ void better(float& bv, int& bi, float v, int i) {
+  if (v > bv || (v == bv && i > bi)) {
+    bv = v;
+    bi = i;
+  }
+}
+
+__global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ logits, int V, int lo, int hi,
+                                                     int suppress_fixed, int min_tokens, const DecodeState* state,
+                                                     int* __restrict__ out, int out_stride) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* lg = logits + (size_t)b * V;
+  const int suppress = state ? (state->step + 1 < min_tokens) : suppress_fixed;
+  float bv = -INFINITY;
+  int bi = -1;
+  for (int i = lo + tid; i < hi; i += 256) {
+    float v = lg[i];
+    if (suppress && i == kEOT) v = -INFINITY;
+    better(bv, bi, v, i);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v = __shfl_xor(bv, o, 64);
+    const int i = __shfl_xor(bi, o, 64);
+    better(bv, bi, v, i);
+  }
+  if (lane == 0) {
+    sv[wave] = bv;
+    si[wave] = bi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w) better(bv, bi, sv[w], si[w]);
+    out[(size_t)b * out_stride] = bi < 0 ? lo : bi;
+  }
+}
+
+hipError_t launch_argmax(const float* logits, int B, int V, int lo, int hi, int suppress_eot,
+                         const DecodeState* state, int* out_tok, int out_stride, hipStream_t st) {
+  hipLaunchKernelGGL(argmax_kernel, dim3(B), dim3(256), 0, st, logits, V, lo, hi, suppress_eot, 0,
+                     (const DecodeState*)nullptr, out_tok, out_stride);
+  (void)state;
+  return hipGetLastError();
+}
+
+hipError_t launch_argmax_step(const float* logits, int B, int V, int min_tokens, const DecodeState* state,
+                              int* out_tok, hipStream_t st) {
+  hipLaunchKernelGGL(argmax_kernel, dim3(B), dim3(256), 0, st, logits, V, 0, V, 0, min_tokens, state, out_tok, 1);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------ bookkeep --
+__global__ void bookkeep_kernel(const int* __restrict__ next, int* __restrict__ tokens, int* __restrict__ ntok,
+                                int* __restrict__ done, int B, int max_tokens, int eot_stop, DecodeState* state) {
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    if (!done[b]) {
+      const int tk = next[b];
+      if (eot_stop && tk == kEOT) {
+        done[b] = 1;
+        atomicAdd(&state->n_done, 1);
+      } else if (ntok[b] < max_tokens) {
+        tokens[(size_t)b * max_tokens + ntok[b]] = tk;
+        ntok[b] += 1;
+      }
+    }
+  }
+  if (threadIdx.x == 0) {
+    state->position += 1;
+    state->kv_len += 1;
+    state->step += 1;
+  }
+}
+
+hipError_t launch_bookkeep(const int* next_tok, int* tokens, int* n_tokens, int* done, int B, int max_tokens,
+                           int eot_stop, DecodeState* state, hipStream_t st) {
+  hipLaunchKernelGGL(bookkeep_kernel, dim3(1), dim3(256), 0, st, next_tok, tokens, n_tokens, done, B, max_tokens,
+                     eot_stop, state);
+  return hipGetLastError();
+}
+
+}  // namespace wa

@@ -1,0 +1,80 @@
+// wa_kernels.hpp -- launchers of the Whisper model kernels around the Q4 path
+// (LayerNorm, attention, conv front-end, embedding, logits, greedy argmax).
+// Reference semantics: src/model/{layers,attention,encoder,decoder,whisper}.rs.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace wa {
+
+// Device-resident decode state (read by kernels, advanced on the device so a
+// captured step graph can be replayed without host involvement).
+struct DecodeState {
+  int position;  // positional-embedding index of the current token
+  int kv_len;    // entries in the self-attention KV cache before this step
+  int step;      // greedy-loop step index (whisper.rs:104)
+  int n_done;    // clips that have emitted EOT
+};
+
+// LayerNorm (layers.rs:23-31, eps 1e-5, biased variance) of rows [M, D].
+// tiled != nullptr: write the A-tiled f16 operand (ns splits) of a Q4 GEMM;
+// else write f32 row-major `out` (ld = D).
+hipError_t launch_layernorm(const float* x, const float* w, const float* b, int M, int D, _Float16* tiled,
+                            int ns, float* out, hipStream_t st);
+
+// Encoder self-attention (attention.rs:243-298, non-causal), flash-style,
+// f32 MFMA.  qkv: [B*T, 3D] f32 (q | k | v).  Writes the A-tiled operand of
+// the output projection (rows b*T + t, K = D).
+hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Float16* tiled, int ns,
+                                    hipStream_t st);
+
+// Decoder self-attention with KV cache (attention.rs:62-125).  qkv [B*Tq, 3D];
+// appends k, v of the Tq new tokens at cache index kv_len (+ kv_base_extra)
+// and attends over kv_len + Tq entries, causal inside the new tokens when
+// Tq > 1 (attention.rs:270-287).  cache_k/v: [B, ctx, D].
+hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float* cache_v, int B, int Tq, int H,
+                                         int ctx, const DecodeState* state, int kv_len_host, _Float16* tiled,
+                                         int ns, hipStream_t st);
+
+// Cross-attention over cached encoder K/V (attention.rs:161-236).  q: [B*Tq,
+// D] f32; kv: [B*T, 2D] f32 (k | v).  Writes the A-tiled operand.
+hipError_t launch_cross_attention(const float* q, const float* kv, int B, int Tq, int T, int H, _Float16* tiled,
+                                  int ns, hipStream_t st);
+
+// Conv1D (layers.rs:77-132) as an implicit-im2col f32 MFMA GEMM + bias +
+// GELU (encoder.rs:89-94) (+ pos[t] if pos != nullptr).  Input element
+// (b, c, t) at in[b*in_bs + c*in_cs + t*in_ts]; output [B, T_out, N].
+// w_t: weights re-laid as [N][3*C] with k = kk*C + c.
+hipError_t launch_conv_gelu(const float* in, long in_bs, long in_cs, long in_ts, int B, int C, int T_in,
+                            int stride, const float* w_t, const float* bias, const float* pos, int N, float* out,
+                            hipStream_t st);
+
+// x[b*Tq + t] = tok_emb[tokens[b*Tq + t]] + pos_emb[pos0 + t]   (decoder.rs:326-343)
+// pos0 = state ? state->position : pos0_host.
+hipError_t launch_embed(const int* tokens, const float* tok_emb, const float* pos_emb, int B, int Tq, int D,
+                        const DecodeState* state, int pos0_host, float* x, hipStream_t st);
+
+// logits[b, v] = h[b * ldh] . E[v]  (decoder.rs:289-292, 342-343), f32
+// products and accumulation (v_mfma_f32_32x32x2_f32).
+hipError_t launch_logits(const float* h, int B, int D, long ldh, const float* emb, int V, float* logits,
+                         hipStream_t st);
+
+// Greedy pick per clip (whisper.rs:119-124, 131-138): argmax with the LAST
+// maximum winning ties (Rust max_by), EOT (50257) masked when suppress != 0,
+// or restricted to [lo, hi) for language detection (whisper.rs:76-83).
+// Writes out_tok[b * out_stride].
+hipError_t launch_argmax(const float* logits, int B, int V, int lo, int hi, int suppress_eot,
+                         const DecodeState* state, int* out_tok, int out_stride, hipStream_t st);
+
+// Greedy-loop bookkeeping at the top of each step (whisper.rs:104-115):
+// for every clip not yet done, EOT -> done (eot_stop != 0), else append the
+// next token; then advance position / kv_len / step.
+hipError_t launch_bookkeep(const int* next_tok, int* tokens, int* n_tokens, int* done, int B, int max_tokens,
+                           int eot_stop, DecodeState* state, hipStream_t st);
+
+// Step-dependent EOT suppression (whisper.rs:120-122) folded into argmax:
+// suppress iff state->step < min_tokens - 1 (state->step already advanced).
+hipError_t launch_argmax_step(const float* logits, int B, int V, int min_tokens, const DecodeState* state,
+                              int* out_tok, hipStream_t st);
+
+}  // namespace wa

@@ -1,0 +1,763 @@
+// wa_model.cpp -- Whisper model runtime around the Q4 path (host side).
+//
+// Re-builds, MI355X-first, the module graph that calls the Q4 operator in the
+// reference (zerr0o/whisper-burn):
+//   WhisperEncoder::forward        src/model/encoder.rs:87-115
+//   EncoderBlock::forward          src/model/encoder.rs:37-49
+//   DecoderBlock::forward_*        src/model/decoder.rs:77-283
+//   WhisperDecoder::forward_prompt src/model/decoder.rs:251-296
+//   WhisperDecoder::decode_step    src/model/decoder.rs:306-348
+//   WhisperModel::transcribe       src/model/whisper.rs:51-128
+// Design points: clips are batched through every kernel; q/k/v
+// (and cross k/v) projections run as ONE Q4 GEMM over row-concatenated Q4
+// weights (bitwise identical per output to separate GEMMs); bias, GELU and
+// the residual add are fused into the Q4 GEMM epilogues; LayerNorm and the
+// attention kernels write the Q4 GEMM operand (A-tiled f16 hi/lo) directly;
+// the KV caches are preallocated (no Tensor::cat); the greedy loop keeps
+// tokens, positions and the done flags on the device and each decode step is
+// one replayed hipGraph.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../../include/whisper_amd.h"
+#include "../../../include/wq4.h"
+#include "wa_kernels.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+wq4_status fail(wq4_status s, const std::string& m) {
+  g_err = m;
+  return s;
+}
+
+#define WA_HIP(expr)                                                                            \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess) return fail(WQ4_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define WA_WQ4(expr)                                                                \
+  do {                                                                              \
+    wq4_status s_ = (expr);                                                         \
+    if (s_ != WQ4_OK) return fail(s_, std::string(#expr) + ": " + wq4_last_error()); \
+  } while (0)
+
+constexpr int kSOT = 50258;
+constexpr int kMaxTokens = 224;  // whisper.rs:20
+constexpr int kMinTokens = 3;    // whisper.rs:97
+
+struct Config {  // WhisperConfig, src/model/config.rs:5-30
+  int n_mels, n_audio_ctx, n_audio_state, n_audio_head, n_audio_layer;
+  int n_text_ctx, n_text_state, n_text_head, n_text_layer, n_vocab, n_lang;
+  int transcribe_token() const { return 50260 + n_lang; }      // config.rs:66-69
+  int no_timestamps_token() const { return transcribe_token() + 4; }  // config.rs:72-74
+};
+
+Config preset(int variant) {
+  switch (variant) {
+    case WA_LARGE_V3:  // config.rs:32-47; vocab = rows of the HF/GGUF embedding
+      return {128, 1500, 1280, 20, 32, 448, 1280, 20, 32, 51866, 100};
+    case WA_MEDIUM:  // config.rs:49-63
+      return {80, 1500, 1024, 16, 24, 448, 1024, 16, 24, 51865, 99};
+    default:  // parity-test configuration (not a released model)
+      return {80, 1500, 384, 6, 2, 448, 384, 6, 2, 51866, 100};
+  }
+}
+
+// ----------------------------------------------- synthetic weights --
+uint64_t fnv1a64(const char* s) {
+  uint64_t h = 0xCBF29CE484222325ull;
+  for (; *s; ++s) {
+    h ^= (uint8_t)*s;
+    h *= 0x100000001B3ull;
+  }
+  return h;
+}
+
+inline uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+template <class F>
+void parallel_for(int64_t n, F fn) {
+  unsigned nt = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+  if (n < (1 << 16)) nt = 1;
+  std::vector<std::thread> th;
+  const int64_t chunk = (n + nt - 1) / nt;
+  for (unsigned t = 0; t < nt; ++t) {
+    const int64_t a = t * chunk, b = std::min(n, a + chunk);
+    if (a >= b) break;
+    th.emplace_back([=] { fn(a, b); });
+  }
+  for (auto& x : th) x.join();
+}
+
+// oracle/oracle.py:synth_uniform -- bit-identical (compiled -ffp-contract=off).
+void synth_uniform(uint64_t seed, const std::string& name, int64_t n, float lo, float hi, float* out) {
+  const uint64_t key = seed ^ fnv1a64(name.c_str());
+  const float span = (float)((double)hi - (double)lo);
+  parallel_for(n, [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) {
+      const float u = (float)(splitmix64(key + (uint64_t)i) >> 40);
+      const float unit = u * (float)(1.0 / 16777216.0);
+      const float t = unit * span;
+      out[i] = lo + t;
+    }
+  });
+}
+
+float lin_scale(int k) { return (float)(1.5 / std::sqrt((double)k)); }
+
+struct Dev {
+  std::vector<void*> ptrs;
+  ~Dev() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  template <class T>
+  T* alloc(size_t n) {
+    void* p = nullptr;
+    if (hipMalloc(&p, n * sizeof(T) + 256) != hipSuccess) return nullptr;
+    ptrs.push_back(p);
+    return static_cast<T*>(p);
+  }
+};
+
+struct EncLayer {
+  float *ln1_w, *ln1_b, *ln2_w, *ln2_b, *qkv_b, *out_b, *fc1_b, *fc2_b;
+  wq4_tensor *qkv = nullptr, *out = nullptr, *fc1 = nullptr, *fc2 = nullptr;
+};
+struct DecLayer {
+  float *ln1_w, *ln1_b, *ln2_w, *ln2_b, *ln3_w, *ln3_b;
+  float *qkv_b, *out_b, *cq_b, *ckv_b, *cout_b, *fc1_b, *fc2_b;
+  wq4_tensor *qkv = nullptr, *out = nullptr, *cq = nullptr, *ckv = nullptr, *cout = nullptr, *fc1 = nullptr,
+             *fc2 = nullptr;
+  float *cache_k, *cache_v, *cross_kv;
+};
+
+}  // namespace
+
+struct wa_model {
+  int device = 0;
+  Config cfg{};
+  wq4_precision prec = WQ4_PREC_F16X2;
+  int ns = 2;
+  int bmax = 1;
+  Dev dev;
+  size_t bytes = 0;
+  // globals
+  float *conv1_wt, *conv1_b, *conv2_wt, *conv2_b, *enc_pos, *lnp_w, *lnp_b;
+  float *tok_emb, *dec_pos, *dln_w, *dln_b;
+  std::vector<EncLayer> enc;
+  std::vector<DecLayer> dec;
+  // activations
+  float *h1, *x, *qkv, *xd, *qkvd, *qd, *hid, *logits;
+  _Float16 *at_d, *at_f, *enc_at, *atd_dec, *atf_dec;
+  int *prompt_tok, *next_tok, *tokens, *ntok, *done;
+  wa::DecodeState* state;
+  int* host_ndone = nullptr;  // pinned ring
+  // step graph
+  hipGraphExec_t graph = nullptr;
+  int graph_b = -1;
+  hipStream_t graph_stream = nullptr;
+  float timings[5] = {0, 0, 0, 0, 0};
+  // live kernel timing (wa_profile_*)
+  struct Pending {
+    hipEvent_t a, b;
+    int cat;
+    double gflop, gb;
+  };
+  bool profile = false;
+  std::vector<Pending> pending;
+  double prof[WA_PROF_CATEGORIES][4] = {};
+
+  void resolve_profile() {
+    for (auto& p : pending) {
+      float ms = 0.0f;
+      if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+        prof[p.cat][0] += 1;
+        prof[p.cat][1] += ms;
+        prof[p.cat][2] += p.gflop;
+        prof[p.cat][3] += p.gb;
+      }
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+    pending.clear();
+  }
+
+  ~wa_model() {
+    resolve_profile();
+    if (graph) (void)hipGraphExecDestroy(graph);
+    if (host_ndone) (void)hipHostFree(host_ndone);
+    for (auto& l : enc)
+      for (wq4_tensor* t : {l.qkv, l.out, l.fc1, l.fc2}) wq4_tensor_destroy(t);
+    for (auto& l : dec)
+      for (wq4_tensor* t : {l.qkv, l.out, l.cq, l.ckv, l.cout, l.fc1, l.fc2}) wq4_tensor_destroy(t);
+  }
+};
+
+namespace {
+
+struct Builder {
+  wa_model* m;
+  uint64_t seed;
+  wq4_status st = WQ4_OK;
+
+  float* upload(const std::vector<float>& v) {
+    float* p = m->dev.alloc<float>(v.size());
+    if (!p || hipMemcpy(p, v.data(), v.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      st = fail(WQ4_ENOMEM, "upload failed");
+      return nullptr;
+    }
+    m->bytes += v.size() * 4;
+    return p;
+  }
+  std::vector<float> gen(const std::string& name, int64_t n, float lo, float hi) {
+    std::vector<float> v((size_t)n);
+    synth_uniform(seed, name, n, lo, hi, v.data());
+    return v;
+  }
+  float* vec(const std::string& name, int64_t n, float lo, float hi) { return upload(gen(name, n, lo, hi)); }
+  // Q4 weights of several GGUF tensors [n_i, k], row-concatenated.
+  wq4_tensor* q4(const std::vector<std::string>& names, const std::vector<int>& rows, int k) {
+    int64_t total = 0;
+    for (int r : rows) total += r;
+    std::vector<uint8_t> raw((size_t)(total * k / 32 * 18));
+    size_t off = 0;
+    for (size_t i = 0; i < names.size(); ++i) {
+      std::vector<float> w = gen(names[i], (int64_t)rows[i] * k, -lin_scale(k), lin_scale(k));
+      const int64_t nblk = (int64_t)rows[i] * k / 32;
+      parallel_for(nblk, [&](int64_t a, int64_t b) {
+        (void)wq4_quantize_q4_0(w.data() + a * 32, (b - a) * 32, raw.data() + off + a * 18);
+      });
+      off += (size_t)nblk * 18;
+    }
+    wq4_tensor* t = nullptr;
+    wq4_status s = wq4_tensor_create(m->device, raw.data(), raw.size(), total, k, &t);
+    if (s != WQ4_OK) st = fail(s, std::string("Q4 upload: ") + wq4_last_error());
+    m->bytes += wq4_tensor_device_bytes(t);
+    return t;
+  }
+  // bias vector of a fused projection: absent biases (attention key) are 0.
+  float* bias_cat(const std::vector<std::string>& names, int n) {
+    std::vector<float> v;
+    for (const auto& nm : names) {
+      if (nm.empty()) {
+        v.insert(v.end(), n, 0.0f);
+      } else {
+        auto b = gen(nm, n, -0.02f, 0.02f);
+        v.insert(v.end(), b.begin(), b.end());
+      }
+    }
+    return upload(v);
+  }
+  // conv weight [N, C, 3] -> [N][kk*C + c] (im2col order, layers.rs:118-121)
+  float* conv(const std::string& name, int N, int C) {
+    auto w = gen(name, (int64_t)N * C * 3, -lin_scale(3 * C), lin_scale(3 * C));
+    std::vector<float> t((size_t)N * 3 * C);
+    for (int n = 0; n < N; ++n)
+      for (int c = 0; c < C; ++c)
+        for (int kk = 0; kk < 3; ++kk) t[(size_t)n * 3 * C + kk * C + c] = w[((size_t)n * C + c) * 3 + kk];
+    return upload(t);
+  }
+};
+
+wq4_status build_synthetic(wa_model* m, uint64_t seed) {
+  const Config& c = m->cfg;
+  const int D = c.n_audio_state, F = 4 * D, Dt = c.n_text_state, Ft = 4 * Dt;
+  Builder B{m, seed};
+  m->conv1_wt = B.conv("encoder.conv1.weight", D, c.n_mels);
+  m->conv1_b = B.vec("encoder.conv1.bias", D, -0.02f, 0.02f);
+  m->conv2_wt = B.conv("encoder.conv2.weight", D, D);
+  m->conv2_b = B.vec("encoder.conv2.bias", D, -0.02f, 0.02f);
+  m->enc_pos = B.vec("encoder.positional_embedding", (int64_t)c.n_audio_ctx * D, -0.1f, 0.1f);
+  m->enc.resize(c.n_audio_layer);
+  for (int i = 0; i < c.n_audio_layer; ++i) {
+    const std::string p = "encoder.blocks." + std::to_string(i);
+    EncLayer& L = m->enc[i];
+    L.ln1_w = B.vec(p + ".attn_ln.weight", D, 0.9f, 1.1f);
+    L.ln1_b = B.vec(p + ".attn_ln.bias", D, -0.05f, 0.05f);
+    L.qkv = B.q4({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, {D, D, D}, D);
+    L.qkv_b = B.bias_cat({p + ".attn.query.bias", "", p + ".attn.value.bias"}, D);
+    L.out = B.q4({p + ".attn.out.weight"}, {D}, D);
+    L.out_b = B.vec(p + ".attn.out.bias", D, -0.02f, 0.02f);
+    L.ln2_w = B.vec(p + ".mlp_ln.weight", D, 0.9f, 1.1f);
+    L.ln2_b = B.vec(p + ".mlp_ln.bias", D, -0.05f, 0.05f);
+    L.fc1 = B.q4({p + ".mlp.0.weight"}, {F}, D);
+    L.fc1_b = B.vec(p + ".mlp.0.bias", F, -0.02f, 0.02f);
+    L.fc2 = B.q4({p + ".mlp.2.weight"}, {D}, F);
+    L.fc2_b = B.vec(p + ".mlp.2.bias", D, -0.02f, 0.02f);
+    if (B.st != WQ4_OK) return B.st;
+  }
+  m->lnp_w = B.vec("encoder.ln_post.weight", D, 0.9f, 1.1f);
+  m->lnp_b = B.vec("encoder.ln_post.bias", D, -0.05f, 0.05f);
+  m->tok_emb = B.vec("decoder.token_embedding.weight", (int64_t)c.n_vocab * Dt, -lin_scale(Dt), lin_scale(Dt));
+  m->dec_pos = B.vec("decoder.positional_embedding", (int64_t)c.n_text_ctx * Dt, -0.02f, 0.02f);
+  m->dec.resize(c.n_text_layer);
+  for (int i = 0; i < c.n_text_layer; ++i) {
+    const std::string p = "decoder.blocks." + std::to_string(i);
+    DecLayer& L = m->dec[i];
+    L.ln1_w = B.vec(p + ".attn_ln.weight", Dt, 0.9f, 1.1f);
+    L.ln1_b = B.vec(p + ".attn_ln.bias", Dt, -0.05f, 0.05f);
+    L.qkv = B.q4({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, {Dt, Dt, Dt}, Dt);
+    L.qkv_b = B.bias_cat({p + ".attn.query.bias", "", p + ".attn.value.bias"}, Dt);
+    L.out = B.q4({p + ".attn.out.weight"}, {Dt}, Dt);
+    L.out_b = B.vec(p + ".attn.out.bias", Dt, -0.02f, 0.02f);
+    L.ln2_w = B.vec(p + ".cross_attn_ln.weight", Dt, 0.9f, 1.1f);
+    L.ln2_b = B.vec(p + ".cross_attn_ln.bias", Dt, -0.05f, 0.05f);
+    L.cq = B.q4({p + ".cross_attn.query.weight"}, {Dt}, Dt);
+    L.cq_b = B.vec(p + ".cross_attn.query.bias", Dt, -0.02f, 0.02f);
+    // cross-attention key has no bias (loader.rs:205-210)
+    L.ckv = B.q4({p + ".cross_attn.key.weight", p + ".cross_attn.value.weight"}, {Dt, Dt}, D);
+    L.ckv_b = B.bias_cat({"", p + ".cross_attn.value.bias"}, Dt);
+    L.cout = B.q4({p + ".cross_attn.out.weight"}, {Dt}, Dt);
+    L.cout_b = B.vec(p + ".cross_attn.out.bias", Dt, -0.02f, 0.02f);
+    L.ln3_w = B.vec(p + ".mlp_ln.weight", Dt, 0.9f, 1.1f);
+    L.ln3_b = B.vec(p + ".mlp_ln.bias", Dt, -0.05f, 0.05f);
+    L.fc1 = B.q4({p + ".mlp.0.weight"}, {Ft}, Dt);
+    L.fc1_b = B.vec(p + ".mlp.0.bias", Ft, -0.02f, 0.02f);
+    L.fc2 = B.q4({p + ".mlp.2.weight"}, {Dt}, Ft);
+    L.fc2_b = B.vec(p + ".mlp.2.bias", Dt, -0.02f, 0.02f);
+    if (B.st != WQ4_OK) return B.st;
+  }
+  m->dln_w = B.vec("decoder.ln.weight", Dt, 0.9f, 1.1f);
+  m->dln_b = B.vec("decoder.ln.bias", Dt, -0.05f, 0.05f);
+  return B.st;
+}
+
+wq4_status alloc_activations(wa_model* m) {
+  const Config& c = m->cfg;
+  const int D = c.n_audio_state, F = 4 * D, Dt = c.n_text_state, Ft = 4 * Dt;
+  const int B = m->bmax, T = c.n_audio_ctx;
+  const int64_t renc = (int64_t)B * T, rdec = (int64_t)B * 4;
+  Dev& d = m->dev;
+  auto tiled = [&](int64_t rows, int k) {
+    const size_t n = wq4_atiled_bytes(rows, k, m->prec);
+    m->bytes += n;
+    return d.alloc<_Float16>(n / 2);
+  };
+  auto f32 = [&](int64_t n) {
+    m->bytes += (size_t)n * 4;
+    return d.alloc<float>((size_t)n);
+  };
+  m->h1 = f32((int64_t)B * 2 * T * D);
+  m->x = f32(renc * D);
+  m->qkv = f32(renc * 3 * D);
+  m->at_d = tiled(renc, D);
+  m->at_f = tiled(renc, F);
+  m->enc_at = tiled(renc, D);
+  for (auto& L : m->dec) {
+    L.cache_k = f32((int64_t)B * c.n_text_ctx * Dt);
+    L.cache_v = f32((int64_t)B * c.n_text_ctx * Dt);
+    L.cross_kv = f32(renc * 2 * Dt);
+  }
+  m->xd = f32(rdec * Dt);
+  m->qkvd = f32(rdec * 3 * Dt);
+  m->qd = f32(rdec * Dt);
+  m->hid = f32(rdec * Dt);
+  m->logits = f32((int64_t)B * c.n_vocab);
+  m->atd_dec = tiled(rdec, Dt);
+  m->atf_dec = tiled(rdec, Ft);
+  m->prompt_tok = d.alloc<int>(rdec);
+  m->next_tok = d.alloc<int>(B);
+  m->tokens = d.alloc<int>((size_t)B * kMaxTokens);
+  m->ntok = d.alloc<int>(B);
+  m->done = d.alloc<int>(B);
+  m->state = d.alloc<wa::DecodeState>(1);
+  for (void* p : {(void*)m->h1, (void*)m->x, (void*)m->qkv, (void*)m->at_d, (void*)m->at_f, (void*)m->enc_at,
+                  (void*)m->xd, (void*)m->qkvd, (void*)m->qd, (void*)m->hid, (void*)m->logits, (void*)m->atd_dec,
+                  (void*)m->atf_dec, (void*)m->prompt_tok, (void*)m->next_tok, (void*)m->tokens, (void*)m->ntok,
+                  (void*)m->done, (void*)m->state})
+    if (!p) return fail(WQ4_ENOMEM, "activation allocation failed");
+  for (auto& L : m->dec)
+    if (!L.cache_k || !L.cache_v || !L.cross_kv) return fail(WQ4_ENOMEM, "KV cache allocation failed");
+  // zero the A-tiled buffers once: padded rows stay finite forever
+  WA_HIP(hipMemset(m->at_d, 0, wq4_atiled_bytes(renc, D, m->prec)));
+  WA_HIP(hipMemset(m->at_f, 0, wq4_atiled_bytes(renc, F, m->prec)));
+  WA_HIP(hipMemset(m->enc_at, 0, wq4_atiled_bytes(renc, D, m->prec)));
+  WA_HIP(hipMemset(m->atd_dec, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
+  WA_HIP(hipMemset(m->atf_dec, 0, wq4_atiled_bytes(rdec, Ft, m->prec)));
+  WA_HIP(hipHostMalloc(reinterpret_cast<void**>(&m->host_ndone), 8 * sizeof(int), 0));
+  return WQ4_OK;
+}
+
+// ------------------------------------------------------------ forward --
+// HIP-event bracket of one launch (only when m->profile).
+struct Prof {
+  wa_model* m;
+  hipStream_t st;
+  int cat;
+  double gflop, gb;
+  hipEvent_t a = nullptr, b = nullptr;
+  Prof(wa_model* m_, hipStream_t st_, int cat_, double gflop_, double gb_)
+      : m(m_), st(st_), cat(cat_), gflop(gflop_), gb(gb_) {
+    if (m->profile && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
+      (void)hipEventRecord(a, st);
+  }
+  ~Prof() {
+    if (a && b) {
+      (void)hipEventRecord(b, st);
+      m->pending.push_back({a, b, cat, gflop, gb});
+    }
+  }
+};
+
+// Algorithmic cost of one Q4 GEMM: 2*rows*N*K flops;
+// N*K*18/32 weight bytes + rows*K*4 (x, f32 at the ABI) + rows*N*4 (y).
+Prof q4prof(wa_model* m, hipStream_t st, const wq4_tensor* w, int64_t rows) {
+  int64_t n = 0, k = 0;
+  (void)wq4_tensor_shape(w, &n, &k);
+  return Prof(m, st, 0, 2.0 * rows * n * k * 1e-9, ((double)n * k * 18 / 32 + 4.0 * rows * k + 4.0 * rows * n) * 1e-9);
+}
+
+// WhisperEncoder::forward (encoder.rs:87-115) + ln_post into the A-tiled
+// operand of the cross-K/V projections.
+wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st, float* enc_out_f32) {
+  const Config& c = m->cfg;
+  const int D = c.n_audio_state, T = c.n_audio_ctx, H = c.n_audio_head;
+  const int T_mel = 2 * T;
+  const int64_t rows = (int64_t)B * T;
+  const double ln_gb = 8.0 * rows * D * 1e-9;
+  {  // conv1 + GELU: mel [B, n_mels, 3000] -> h1 [B, 3000, D]   (encoder.rs:89-90)
+    Prof p(m, st, 2, 2.0 * B * T_mel * D * 3.0 * c.n_mels * 1e-9, 4.0 * B * T_mel * (c.n_mels + D) * 1e-9);
+    WA_HIP(wa::launch_conv_gelu(mel, (long)c.n_mels * T_mel, T_mel, 1, B, c.n_mels, T_mel, 1, m->conv1_wt,
+                                m->conv1_b, nullptr, D, m->h1, st));
+  }
+  {  // conv2 (stride 2) + GELU + positional embedding -> x [B, 1500, D]   (:93-106)
+    Prof p(m, st, 2, 2.0 * rows * D * 3.0 * D * 1e-9, 4.0 * B * (T_mel + T) * D * 1e-9);
+    WA_HIP(wa::launch_conv_gelu(m->h1, (long)T_mel * D, 1, D, B, D, T_mel, 2, m->conv2_wt, m->conv2_b, m->enc_pos,
+                                D, m->x, st));
+  }
+  for (auto& L : m->enc) {  // EncoderBlock::forward (encoder.rs:37-49)
+    {
+      Prof p(m, st, 3, 0.0, ln_gb);
+      WA_HIP(wa::launch_layernorm(m->x, L.ln1_w, L.ln1_b, (int)rows, D, m->at_d, m->ns, nullptr, st));
+    }
+    {
+      Prof p = q4prof(m, st, L.qkv, rows);
+      WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, m->at_d, nullptr, m->qkv, nullptr, rows, 0u, m->prec, 1, st));
+    }
+    {
+      Prof p(m, st, 1, 4.0 * B * H * (double)T * T * 64 * 1e-9, 16.0 * rows * D * 1e-9);
+      WA_HIP(wa::launch_encoder_attention(m->qkv, B, T, H, m->at_d, m->ns, st));
+    }
+    {
+      Prof p = q4prof(m, st, L.out, rows);
+      WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, m->at_d, m->x, m->x, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 1, st));
+    }
+    {
+      Prof p(m, st, 3, 0.0, ln_gb);
+      WA_HIP(wa::launch_layernorm(m->x, L.ln2_w, L.ln2_b, (int)rows, D, m->at_d, m->ns, nullptr, st));
+    }
+    {
+      Prof p = q4prof(m, st, L.fc1, rows);
+      WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, m->at_d, nullptr, nullptr, m->at_f, rows,
+                            WQ4_EPI_GELU | WQ4_EPI_TILED_OUT, m->prec, 1, st));
+    }
+    {
+      Prof p = q4prof(m, st, L.fc2, rows);
+      WA_WQ4(wq4_gemm_tiled(L.fc2, L.fc2_b, m->at_f, m->x, m->x, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 1, st));
+    }
+  }
+  {
+    Prof p(m, st, 3, 0.0, ln_gb);
+    WA_HIP(wa::launch_layernorm(m->x, m->lnp_w, m->lnp_b, (int)rows, D, m->enc_at, m->ns, nullptr, st));
+  }
+  if (enc_out_f32) WA_HIP(wa::launch_layernorm(m->x, m->lnp_w, m->lnp_b, (int)rows, D, nullptr, 2, enc_out_f32, st));
+  return WQ4_OK;
+}
+
+// Cross-attention K/V of every decoder layer from encoder_out
+// (attention.rs:309-335 forward_init_cache, run once per clip).
+wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st) {
+  const int64_t rows = (int64_t)B * m->cfg.n_audio_ctx;
+  for (auto& L : m->dec) {
+    Prof p = q4prof(m, st, L.ckv, rows);
+    WA_WQ4(wq4_gemm_tiled(L.ckv, L.ckv_b, m->enc_at, nullptr, L.cross_kv, nullptr, rows, 0u, m->prec, 1, st));
+  }
+  return WQ4_OK;
+}
+
+// Decoder pass over Tq new tokens per clip (forward_prompt when state ==
+// nullptr, decode_step otherwise), ending in last-position logits.
+wq4_status decoder_forward(wa_model* m, const int* tokens, int B, int Tq, const wa::DecodeState* state, int pos0,
+                           int kv0, hipStream_t st) {
+  const Config& c = m->cfg;
+  const int D = c.n_text_state, H = c.n_text_head;
+  const int64_t rows = (int64_t)B * Tq;
+  WA_HIP(wa::launch_embed(tokens, m->tok_emb, m->dec_pos, B, Tq, D, state, pos0, m->xd, st));
+  for (auto& L : m->dec) {  // DecoderBlock (decoder.rs:77-112 / 140-183)
+    WA_HIP(wa::launch_layernorm(m->xd, L.ln1_w, L.ln1_b, (int)rows, D, m->atd_dec, m->ns, nullptr, st));
+    WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, m->atd_dec, nullptr, m->qkvd, nullptr, rows, 0u, m->prec, 2, st));
+    WA_HIP(wa::launch_decoder_self_attention(m->qkvd, L.cache_k, L.cache_v, B, Tq, H, c.n_text_ctx, state, kv0,
+                                             m->atd_dec, m->ns, st));
+    WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, m->atd_dec, m->xd, m->xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
+    WA_HIP(wa::launch_layernorm(m->xd, L.ln2_w, L.ln2_b, (int)rows, D, m->atd_dec, m->ns, nullptr, st));
+    WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, m->atd_dec, nullptr, m->qd, nullptr, rows, 0u, m->prec, 2, st));
+    WA_HIP(wa::launch_cross_attention(m->qd, L.cross_kv, B, Tq, c.n_audio_ctx, H, m->atd_dec, m->ns, st));
+    WA_WQ4(wq4_gemm_tiled(L.cout, L.cout_b, m->atd_dec, m->xd, m->xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2,
+                          st));
+    WA_HIP(wa::launch_layernorm(m->xd, L.ln3_w, L.ln3_b, (int)rows, D, m->atd_dec, m->ns, nullptr, st));
+    WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, m->atd_dec, nullptr, nullptr, m->atf_dec, rows,
+                          WQ4_EPI_GELU | WQ4_EPI_TILED_OUT, m->prec, 2, st));
+    WA_WQ4(wq4_gemm_tiled(L.fc2, L.fc2_b, m->atf_dec, m->xd, m->xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
+  }
+  // final LN (decoder.rs:286 / 340) and tied-embedding logits of the last
+  // position of every clip (decoder.rs:289-292, 342-343)
+  WA_HIP(wa::launch_layernorm(m->xd, m->dln_w, m->dln_b, (int)rows, D, nullptr, 2, m->hid, st));
+  WA_HIP(wa::launch_logits(m->hid + (size_t)(Tq - 1) * D, B, D, (int64_t)Tq * D, m->tok_emb, c.n_vocab, m->logits,
+                           st));
+  return WQ4_OK;
+}
+
+// One greedy step (whisper.rs:104-125): bookkeeping, decode_step, argmax.
+wq4_status decode_step(wa_model* m, int B, int eot_stop, hipStream_t st) {
+  WA_HIP(wa::launch_bookkeep(m->next_tok, m->tokens, m->ntok, m->done, B, kMaxTokens, eot_stop, m->state, st));
+  wq4_status s = decoder_forward(m, m->next_tok, B, 1, m->state, 0, 0, st);
+  if (s != WQ4_OK) return s;
+  WA_HIP(wa::launch_argmax_step(m->logits, B, m->cfg.n_vocab, kMinTokens, m->state, m->next_tok, st));
+  return WQ4_OK;
+}
+
+}  // namespace
+
+// ================================================================= C ABI ==
+extern "C" {
+
+const char* wa_last_error(void) { return g_err.c_str(); }
+
+wq4_status wa_synth_uniform(uint64_t seed, const char* name, int64_t n, float lo, float hi, float* out) {
+  if (!name || !out || n < 0) return fail(WQ4_EINVAL, "bad argument");
+  synth_uniform(seed, name, n, lo, hi, out);
+  return WQ4_OK;
+}
+
+wq4_status wa_model_create_synthetic(int device, int variant, uint64_t seed, int max_batch, wq4_precision prec,
+                                     wa_model** out) {
+  if (!out) return fail(WQ4_EINVAL, "out is null");
+  *out = nullptr;
+  if (variant < 0 || variant > 2) return fail(WQ4_EINVAL, "unknown variant");
+  if (max_batch < 1 || max_batch > 256) return fail(WQ4_EINVAL, "max_batch must be in [1, 256]");
+  if (prec != WQ4_PREC_F16X2 && prec != WQ4_PREC_F16) return fail(WQ4_EINVAL, "unknown precision");
+  WA_HIP(hipSetDevice(device));
+  std::unique_ptr<wa_model> m(new wa_model());
+  m->device = device;
+  m->cfg = preset(variant);
+  m->prec = prec;
+  m->ns = prec == WQ4_PREC_F16 ? 1 : 2;
+  m->bmax = max_batch;
+  wq4_status s = build_synthetic(m.get(), seed);
+  if (s != WQ4_OK) return s;
+  s = alloc_activations(m.get());
+  if (s != WQ4_OK) return s;
+  *out = m.release();
+  return WQ4_OK;
+}
+
+void wa_model_destroy(wa_model* m) { delete m; }
+
+wq4_status wa_model_config(const wa_model* m, int32_t* cfg) {
+  if (!m || !cfg) return fail(WQ4_EINVAL, "null argument");
+  const Config& c = m->cfg;
+  const int32_t v[WA_CFG_COUNT] = {c.n_mels,       c.n_audio_ctx,  c.n_audio_state, c.n_audio_head,
+                                   c.n_audio_layer, c.n_text_ctx,   c.n_text_state,  c.n_text_head,
+                                   c.n_text_layer,  c.n_vocab,      c.n_lang};
+  std::memcpy(cfg, v, sizeof(v));
+  return WQ4_OK;
+}
+
+size_t wa_model_device_bytes(const wa_model* m) { return m ? m->bytes : 0; }
+
+wq4_status wa_last_timings(const wa_model* m, float* out) {
+  if (!m || !out) return fail(WQ4_EINVAL, "null argument");
+  std::memcpy(out, m->timings, sizeof(m->timings));
+  return WQ4_OK;
+}
+
+wq4_status wa_profile_enable(wa_model* m, int enable) {
+  if (!m) return fail(WQ4_EINVAL, "null model");
+  m->profile = enable != 0;
+  return WQ4_OK;
+}
+
+wq4_status wa_profile_read(wa_model* m, double* out, int reset) {
+  if (!m || !out) return fail(WQ4_EINVAL, "null argument");
+  m->resolve_profile();
+  std::memcpy(out, m->prof, sizeof(m->prof));
+  if (reset) std::memset(m->prof, 0, sizeof(m->prof));
+  return WQ4_OK;
+}
+
+wq4_status wa_encode(wa_model* m, const float* mel_dev, int n_clips, float* enc_out_dev, void* stream) {
+  if (!m || !mel_dev) return fail(WQ4_EINVAL, "null argument");
+  if (n_clips < 1 || n_clips > m->bmax) return fail(WQ4_EINVAL, "n_clips out of range");
+  WA_HIP(hipSetDevice(m->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  wq4_status s = encoder_forward(m, mel_dev, n_clips, st, enc_out_dev);
+  if (s != WQ4_OK) return s;
+  return cross_kv_forward(m, n_clips, st);
+}
+
+wq4_status wa_prompt_logits(wa_model* m, const int32_t* prompt_dev, int n_clips, int plen, float* logits_dev,
+                            void* stream) {
+  if (!m || !prompt_dev || !logits_dev) return fail(WQ4_EINVAL, "null argument");
+  if (n_clips < 1 || n_clips > m->bmax || plen < 1 || plen > 4) return fail(WQ4_EINVAL, "bad n_clips / plen");
+  WA_HIP(hipSetDevice(m->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  wq4_status s = decoder_forward(m, prompt_dev, n_clips, plen, nullptr, 0, 0, st);
+  if (s != WQ4_OK) return s;
+  WA_HIP(hipMemcpyAsync(logits_dev, m->logits, (size_t)n_clips * m->cfg.n_vocab * 4, hipMemcpyDeviceToDevice, st));
+  return WQ4_OK;
+}
+
+wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lang_token, int max_tokens,
+                         int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out, void* stream) {
+  if (!m || !mel_dev || !tokens_out || !n_tokens_out) return fail(WQ4_EINVAL, "null argument");
+  if (n_clips < 1 || n_clips > m->bmax) return fail(WQ4_EINVAL, "n_clips out of range");
+  if (max_tokens < 1 || max_tokens > kMaxTokens) return fail(WQ4_EINVAL, "max_tokens must be in [1, 224]");
+  WA_HIP(hipSetDevice(m->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const Config& c = m->cfg;
+  const int B = n_clips;
+  hipEvent_t ev[5];
+  for (auto& e : ev) WA_HIP(hipEventCreate(&e));
+  struct EvGuard {
+    hipEvent_t* e;
+    ~EvGuard() {
+      for (int i = 0; i < 5; ++i) (void)hipEventDestroy(e[i]);
+    }
+  } evg{ev};
+
+  WA_HIP(hipEventRecord(ev[0], st));
+  wq4_status s = encoder_forward(m, mel_dev, B, st, nullptr);
+  if (s != WQ4_OK) return s;
+  WA_HIP(hipEventRecord(ev[1], st));
+  s = cross_kv_forward(m, B, st);
+  if (s != WQ4_OK) return s;
+  WA_HIP(hipEventRecord(ev[2], st));
+
+  // prompt (whisper.rs:60-99)
+  std::vector<int> ptok((size_t)B * 4);
+  int pos0, kv0;
+  if (lang_token >= 0) {
+    for (int b = 0; b < B; ++b) {
+      ptok[b * 4 + 0] = kSOT;
+      ptok[b * 4 + 1] = lang_token;
+      ptok[b * 4 + 2] = c.transcribe_token();
+      ptok[b * 4 + 3] = c.no_timestamps_token();
+    }
+    WA_HIP(hipMemcpyAsync(m->prompt_tok, ptok.data(), (size_t)B * 4 * 4, hipMemcpyHostToDevice, st));
+    s = decoder_forward(m, m->prompt_tok, B, 4, nullptr, 0, 0, st);
+    if (s != WQ4_OK) return s;
+    pos0 = 4;
+    kv0 = 4;
+  } else {
+    // decode_step(SOT, 0) fills a 1-entry cache; the language is the last max
+    // over the language-token range (whisper.rs:73-83) ...
+    for (int b = 0; b < B; ++b) {
+      ptok[b * 3 + 0] = kSOT;
+      ptok[b * 3 + 1] = c.transcribe_token();
+      ptok[b * 3 + 2] = c.no_timestamps_token();
+    }
+    WA_HIP(hipMemcpyAsync(m->prompt_tok, ptok.data(), (size_t)B * 3 * 4, hipMemcpyHostToDevice, st));
+    // SOT rows: prompt_tok[b*3] (embed reads tokens[b*Tq + t] with Tq = 1 ->
+    // needs a contiguous [B] array: use next_tok as scratch)
+    std::vector<int> sot(B, kSOT);
+    WA_HIP(hipMemcpyAsync(m->next_tok, sot.data(), (size_t)B * 4, hipMemcpyHostToDevice, st));
+    s = decoder_forward(m, m->next_tok, B, 1, nullptr, 0, 0, st);
+    if (s != WQ4_OK) return s;
+    WA_HIP(wa::launch_argmax(m->logits, B, c.n_vocab, 50259, 50259 + c.n_lang, 0, nullptr, m->prompt_tok, 3, st));
+    // ... then forward_prompt([lang, TRANSCRIBE, NO_TIMESTAMPS]) OVERWRITES the
+    // cache from index 0 with positions 0..2 (decoder.rs:272-283) while the
+    // position counter continues at 1 + 3 = 4 (whisper.rs:74,93).
+    s = decoder_forward(m, m->prompt_tok, B, 3, nullptr, 0, 0, st);
+    if (s != WQ4_OK) return s;
+    pos0 = 4;
+    kv0 = 3;
+  }
+  // first token: EOT suppressed (whisper.rs:97-99)
+  WA_HIP(wa::launch_argmax(m->logits, B, c.n_vocab, 0, c.n_vocab, 1, nullptr, m->next_tok, 1, st));
+  const wa::DecodeState init{pos0 - 1, kv0 - 1, -1, 0};
+  WA_HIP(hipMemcpyAsync(m->state, &init, sizeof(init), hipMemcpyHostToDevice, st));
+  WA_HIP(hipMemsetAsync(m->ntok, 0, (size_t)B * 4, st));
+  WA_HIP(hipMemsetAsync(m->done, 0, (size_t)B * 4, st));
+  WA_HIP(hipMemsetAsync(m->tokens, 0, (size_t)B * kMaxTokens * 4, st));
+  WA_HIP(hipEventRecord(ev[3], st));
+
+  // greedy loop (whisper.rs:104-125), one replayed graph per step
+  if (!m->graph || m->graph_b != B * 2 + (eot_stop ? 1 : 0) || m->graph_stream != st) {
+    if (m->graph) {
+      (void)hipGraphExecDestroy(m->graph);
+      m->graph = nullptr;
+    }
+    hipGraph_t g;
+    WA_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    s = decode_step(m, B, eot_stop, st);
+    hipError_t ce = hipStreamEndCapture(st, &g);
+    if (s != WQ4_OK) return s;
+    if (ce != hipSuccess) return fail(WQ4_EHIP, std::string("graph capture: ") + hipGetErrorString(ce));
+    ce = hipGraphInstantiate(&m->graph, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ce != hipSuccess) return fail(WQ4_EHIP, std::string("graph instantiate: ") + hipGetErrorString(ce));
+    m->graph_b = B * 2 + (eot_stop ? 1 : 0);
+    m->graph_stream = st;
+  }
+  hipEvent_t ring[8];
+  for (auto& e : ring) WA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  struct RingGuard {
+    hipEvent_t* e;
+    ~RingGuard() {
+      for (int i = 0; i < 8; ++i) (void)hipEventDestroy(e[i]);
+    }
+  } rg{ring};
+  int steps = 0;
+  const int lag = 4;
+  for (int step = 0; step < max_tokens; ++step) {
+    WA_HIP(hipGraphLaunch(m->graph, st));
+    ++steps;
+    if (eot_stop) {
+      const int slot = step % 8;
+      WA_HIP(hipMemcpyAsync(&m->host_ndone[slot], &m->state->n_done, sizeof(int), hipMemcpyDeviceToHost, st));
+      WA_HIP(hipEventRecord(ring[slot], st));
+      if (step >= lag) {
+        const int old = (step - lag) % 8;
+        WA_HIP(hipEventSynchronize(ring[old]));
+        if (m->host_ndone[old] >= B) break;  // every clip had emitted EOT by then
+      }
+    }
+  }
+  // the loop's bookkeeping for tokens chosen by the last step happens at the
+  // top of a step that the reference never runs: nothing to add.
+  WA_HIP(hipEventRecord(ev[4], st));
+  std::vector<int32_t> tok((size_t)B * kMaxTokens), nt(B);
+  WA_HIP(hipMemcpyAsync(tok.data(), m->tokens, tok.size() * 4, hipMemcpyDeviceToHost, st));
+  WA_HIP(hipMemcpyAsync(nt.data(), m->ntok, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+  WA_HIP(hipStreamSynchronize(st));
+  for (int b = 0; b < B; ++b) {
+    n_tokens_out[b] = std::min(nt[b], max_tokens);
+    std::memcpy(tokens_out + (size_t)b * max_tokens, tok.data() + (size_t)b * kMaxTokens,
+                (size_t)max_tokens * 4);
+  }
+  float ms[4];
+  for (int i = 0; i < 4; ++i) WA_HIP(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
+  m->timings[0] = ms[0];
+  m->timings[1] = ms[1];
+  m->timings[2] = ms[2];
+  m->timings[3] = ms[3];
+  m->timings[4] = (float)steps;
+  return WQ4_OK;
+}
+
+}  // extern "C"

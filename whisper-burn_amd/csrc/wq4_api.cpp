@@ -10,9 +10,10 @@
 // status codes instead of panics.
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
-#include <atomic>
 #include <map>
 #include <mutex>
 #include <string>
@@ -26,8 +27,12 @@
 struct wq4_tensor {
   int device = 0;
   wq4::Q4Geom g;
-  uint8_t* nib = nullptr;   // device, g.nib_bytes()
-  uint32_t* sc = nullptr;   // device, g.sc_bytes()
+  bool flat = false;         // K % 32 != 0: stored as raw blocks, no GEMM (see create)
+  uint8_t* nib = nullptr;    // device, g.nib_bytes()
+  uint32_t* sc = nullptr;    // device, g.sc_bytes()
+  float* cs = nullptr;       // device, g.colscale_bytes()
+  uint8_t* raw = nullptr;    // device, raw GGUF bytes (flat tensors only)
+  size_t raw_bytes = 0;
 };
 
 namespace {
@@ -116,6 +121,19 @@ wq4_status check_prec(wq4_precision p) {
   return WQ4_OK;
 }
 
+wq4_status check_gemm_tensor(const wq4_tensor* w) {
+  if (!w) return fail(WQ4_EINVAL, "weights are null");
+  if (w->flat)  // the reference shader needs whole blocks per row (shader.wgsl:69)
+    return fail(WQ4_ESHAPE, "q4_matmul needs K % 32 == 0, weights are [" + std::to_string(w->g.n) + ", " +
+                                std::to_string(w->g.k) + "]");
+  return WQ4_OK;
+}
+
+hipError_t gemm(const wq4_tensor* w, const _Float16* at, int64_t rows, const wq4::EpiArgs& e, int mode, int ns,
+                hipStream_t st) {
+  return wq4::launch_q4_gemm(w->g, w->nib, w->sc, w->cs, at, (int)rows, e, mode, ns, use_decode(rows), st);
+}
+
 }  // namespace
 
 extern "C" {
@@ -153,13 +171,11 @@ wq4_status wq4_tensor_create(int device, const uint8_t* raw, size_t nbytes, int6
                              wq4_tensor** out) {
   if (!out) return fail(WQ4_EINVAL, "out is null");
   *out = nullptr;
-  if (n <= 0 || k <= 0) return fail(WQ4_ESHAPE, "Q4_0 shape must be positive, got [" + std::to_string(n) + ", " +
-                                                    std::to_string(k) + "]");
+  if (n <= 0 || k <= 0)
+    return fail(WQ4_ESHAPE, "Q4_0 shape must be positive, got [" + std::to_string(n) + ", " + std::to_string(k) + "]");
   const int64_t elems = n * k;
   if (elems % 32 != 0)  // tensor.rs:38-42
     return fail(WQ4_ESHAPE, "Q4_0 requires element count divisible by 32, got " + std::to_string(elems));
-  if (k % 32 != 0)  // shader.wgsl:69 assumes it; the reference never checks
-    return fail(WQ4_ESHAPE, "Q4_0 rows must hold whole blocks: K % 32 != 0 (K = " + std::to_string(k) + ")");
   const int64_t nblocks = elems / 32;
   const size_t expected = (size_t)nblocks * 18;
   if (nbytes != expected)  // tensor.rs:43-48
@@ -173,13 +189,26 @@ wq4_status wq4_tensor_create(int device, const uint8_t* raw, size_t nbytes, int6
   auto* t = new wq4_tensor();
   t->device = device;
   t->g = wq4::make_geom(n, k);
-  std::vector<uint8_t> nib(t->g.nib_bytes());
-  std::vector<uint32_t> sc(t->g.sc_bytes() / 4);
-  wq4::repack_q4(raw, t->g, nib.data(), sc.data());
-  hipError_t e = hipMalloc(&t->nib, nib.size());
-  if (e == hipSuccess) e = hipMalloc(&t->sc, t->g.sc_bytes());
-  if (e == hipSuccess) e = hipMemcpy(t->nib, nib.data(), nib.size(), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(t->sc, sc.data(), t->g.sc_bytes(), hipMemcpyHostToDevice);
+  hipError_t e = hipSuccess;
+  if (k % 32 != 0) {
+    // Accepted like the reference (only N*K % 32 is checked, tensor.rs:38-42)
+    // and kept as raw blocks: dequantize() works, GEMM entry points refuse.
+    t->flat = true;
+    t->raw_bytes = nbytes;
+    e = hipMalloc(&t->raw, nbytes);
+    if (e == hipSuccess) e = hipMemcpy(t->raw, raw, nbytes, hipMemcpyHostToDevice);
+  } else {
+    std::vector<uint8_t> nib(t->g.nib_bytes());
+    std::vector<uint32_t> sc(t->g.sc_bytes() / 4);
+    std::vector<float> cs(t->g.np);
+    wq4::repack_q4(raw, t->g, nib.data(), sc.data(), cs.data());
+    e = hipMalloc(&t->nib, nib.size());
+    if (e == hipSuccess) e = hipMalloc(&t->sc, t->g.sc_bytes());
+    if (e == hipSuccess) e = hipMalloc(&t->cs, t->g.colscale_bytes());
+    if (e == hipSuccess) e = hipMemcpy(t->nib, nib.data(), nib.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(t->sc, sc.data(), t->g.sc_bytes(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(t->cs, cs.data(), t->g.colscale_bytes(), hipMemcpyHostToDevice);
+  }
   if (e != hipSuccess) {
     wq4_tensor_destroy(t);
     return hip_fail(e, "Q4Tensor upload");
@@ -193,6 +222,8 @@ void wq4_tensor_destroy(wq4_tensor* t) {
   DeviceGuard dg(t->device);
   if (t->nib) (void)hipFree(t->nib);
   if (t->sc) (void)hipFree(t->sc);
+  if (t->cs) (void)hipFree(t->cs);
+  if (t->raw) (void)hipFree(t->raw);
   delete t;
 }
 
@@ -203,19 +234,28 @@ wq4_status wq4_tensor_shape(const wq4_tensor* t, int64_t* n, int64_t* k) {
   return WQ4_OK;
 }
 
-int64_t wq4_tensor_num_blocks(const wq4_tensor* t) { return t ? t->g.n * t->g.kb : -1; }
+int64_t wq4_tensor_num_blocks(const wq4_tensor* t) { return t ? t->g.n * t->g.k / 32 : -1; }
 int wq4_tensor_device(const wq4_tensor* t) { return t ? t->device : -1; }
-size_t wq4_tensor_device_bytes(const wq4_tensor* t) { return t ? t->g.nib_bytes() + t->g.sc_bytes() : 0; }
+size_t wq4_tensor_device_bytes(const wq4_tensor* t) {
+  if (!t) return 0;
+  return t->flat ? t->raw_bytes : t->g.nib_bytes() + t->g.sc_bytes() + t->g.colscale_bytes();
+}
 
 wq4_status wq4_tensor_raw_bytes(const wq4_tensor* t, uint8_t* host_out) {
   if (!t || !host_out) return fail(WQ4_EINVAL, "null argument");
   DeviceGuard dg(t->device);
+  if (t->flat) {
+    hipError_t e = hipMemcpy(host_out, t->raw, t->raw_bytes, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? WQ4_OK : hip_fail(e, "Q4Tensor read-back");
+  }
   std::vector<uint8_t> nib(t->g.nib_bytes());
   std::vector<uint32_t> sc(t->g.sc_bytes() / 4);
+  std::vector<float> cs(t->g.np);
   hipError_t e = hipMemcpy(nib.data(), t->nib, nib.size(), hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(sc.data(), t->sc, t->g.sc_bytes(), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(cs.data(), t->cs, t->g.colscale_bytes(), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return hip_fail(e, "Q4Tensor read-back");
-  wq4::unrepack_q4(nib.data(), sc.data(), t->g, host_out);
+  wq4::unrepack_q4(nib.data(), sc.data(), cs.data(), t->g, host_out);
   return WQ4_OK;
 }
 
@@ -224,10 +264,10 @@ static float f16_to_f32_host(uint16_t h) { return (float)__builtin_bit_cast(_Flo
 // Q4Tensor::dequantize, src/gguf/tensor.rs:88-113 (D2H, then host dequant).
 wq4_status wq4_tensor_dequantize(const wq4_tensor* t, float* host_out) {
   if (!t || !host_out) return fail(WQ4_EINVAL, "null argument");
-  std::vector<uint8_t> raw((size_t)t->g.n * t->g.kb * 18);
+  const int64_t nb = t->g.n * t->g.k / 32;
+  std::vector<uint8_t> raw((size_t)nb * 18);
   wq4_status s = wq4_tensor_raw_bytes(t, raw.data());
   if (s != WQ4_OK) return s;
-  const int64_t nb = t->g.n * t->g.kb;
   for (int64_t b = 0; b < nb; ++b) {
     const uint8_t* o = raw.data() + b * 18;
     const float d = f16_to_f32_host((uint16_t)(o[0] | (o[1] << 8)));
@@ -243,31 +283,32 @@ wq4_status wq4_tensor_dequantize(const wq4_tensor* t, float* host_out) {
 }
 
 size_t wq4_linear_workspace_bytes(const wq4_tensor* w, int64_t rows) {
-  if (!w) return 0;
+  if (!w || w->flat) return 0;
   return wq4::atiled_bytes(rows, w->g.k, 2);
 }
 
 size_t wq4_ffn_workspace_bytes(const wq4_tensor* fc1, const wq4_tensor* fc2, int64_t rows) {
-  if (!fc1 || !fc2) return 0;
+  if (!fc1 || !fc2 || fc1->flat || fc2->flat) return 0;
   return wq4::atiled_bytes(rows, fc1->g.k, 2) + wq4::atiled_bytes(rows, fc2->g.k, 2);
 }
 
 static wq4_status linear_impl(const wq4_tensor* w, const float* bias, const float* x, const float* residual,
                               float* y, int64_t rows, int64_t k, unsigned flags, wq4_precision prec, void* ws,
                               size_t ws_bytes, void* stream) {
-  if (!w || !x || !y) return fail(WQ4_EINVAL, "null argument");
-  wq4_status s = check_prec(prec);
+  wq4_status s = check_gemm_tensor(w);
+  if (s != WQ4_OK) return s;
+  s = check_prec(prec);
   if (s != WQ4_OK) return s;
   if (k != w->g.k)  // op.rs:58-61
     return fail(WQ4_ESHAPE, "K dimension mismatch: input has " + std::to_string(k) + ", weights have " +
                                 std::to_string(w->g.k));
   if (rows < 0 || rows > (1 << 24)) return fail(WQ4_ESHAPE, "bad row count " + std::to_string(rows));
+  if (rows == 0) return WQ4_OK;  // empty batch: nothing to read or write
+  if (!x || !y) return fail(WQ4_EINVAL, "null activation / output pointer");
   if ((flags & WQ4_EPI_RESIDUAL) && !residual) return fail(WQ4_EINVAL, "WQ4_EPI_RESIDUAL without residual");
-  if (rows == 0) return WQ4_OK;
   const int ns = ns_of(prec);
   const size_t need = wq4::atiled_bytes(rows, k, ns);
-  if (!ws || ws_bytes < need)
-    return fail(WQ4_ENOMEM, "workspace too small: need " + std::to_string(need) + " bytes");
+  if (!ws || ws_bytes < need) return fail(WQ4_ENOMEM, "workspace too small: need " + std::to_string(need) + " bytes");
   DeviceGuard dg(w->device);
   if (!dg.ok) return fail(WQ4_EHIP, "hipSetDevice failed");
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -276,7 +317,7 @@ static wq4_status linear_impl(const wq4_tensor* w, const float* bias, const floa
   if (e != hipSuccess) return hip_fail(e, "tile_activations launch");
   wq4::EpiArgs epi = make_epi(bias, (flags & WQ4_EPI_RESIDUAL) ? residual : nullptr, y, (int)w->g.n, (int)rows,
                               (int)w->g.n, (flags & WQ4_EPI_GELU) != 0);
-  e = wq4::launch_q4_gemm(w->g, w->nib, w->sc, at, (int)rows, epi, wq4::kEpiF32, ns, use_decode(rows), st);
+  e = gemm(w, at, rows, epi, wq4::kEpiF32, ns, st);
   if (e != hipSuccess) return hip_fail(e, "q4_gemm launch");
   return WQ4_OK;
 }
@@ -289,15 +330,16 @@ wq4_status wq4_linear_forward_ws(const wq4_tensor* w, const float* bias_dev, con
 
 wq4_status wq4_linear_forward(const wq4_tensor* w, const float* bias_dev, const float* x_dev, float* y_dev,
                               int64_t b, int64_t m, int64_t k, void* stream) {
-  if (!w) return fail(WQ4_EINVAL, "weights are null");
+  wq4_status s = check_gemm_tensor(w);
+  if (s != WQ4_OK) return s;
   if (b < 0 || m < 0) return fail(WQ4_ESHAPE, "negative B or M");
   const int64_t rows = b * m;
   const wq4_precision prec = wq4_get_precision();
   void* ws = nullptr;
-  const size_t need = wq4::atiled_bytes(rows, k, ns_of(prec));
-  {
+  const size_t need = wq4::atiled_bytes(rows, k > 0 ? k : 32, ns_of(prec));
+  if (rows > 0 && k == w->g.k) {
     DeviceGuard dg(w->device);
-    wq4_status s = arena_get(w->device, stream, need, &ws);
+    s = arena_get(w->device, stream, need, &ws);
     if (s != WQ4_OK) return s;
   }
   return linear_impl(w, bias_dev, x_dev, nullptr, y_dev, rows, k, 0u, prec, ws, need, stream);
@@ -312,17 +354,20 @@ wq4_status wq4_matmul(const wq4_tensor* w, const float* x_dev, float* y_dev, int
 static wq4_status ffn_impl(const wq4_tensor* fc1, const float* b1, const wq4_tensor* fc2, const float* b2,
                            const float* x, const float* residual, float* y, int64_t rows, unsigned flags,
                            wq4_precision prec, void* ws, size_t ws_bytes, void* stream) {
-  if (!fc1 || !fc2 || !x || !y) return fail(WQ4_EINVAL, "null argument");
-  wq4_status s = check_prec(prec);
+  wq4_status s = check_gemm_tensor(fc1);
+  if (s == WQ4_OK) s = check_gemm_tensor(fc2);
+  if (s != WQ4_OK) return s;
+  s = check_prec(prec);
   if (s != WQ4_OK) return s;
   if (fc1->device != fc2->device) return fail(WQ4_EINVAL, "fc1 and fc2 live on different devices");
   if (fc2->g.k != fc1->g.n)
     return fail(WQ4_ESHAPE, "FFN shape mismatch: fc1 is [" + std::to_string(fc1->g.n) + ", " +
                                 std::to_string(fc1->g.k) + "], fc2 is [" + std::to_string(fc2->g.n) + ", " +
                                 std::to_string(fc2->g.k) + "]");
-  if ((flags & WQ4_EPI_RESIDUAL) && !residual) return fail(WQ4_EINVAL, "WQ4_EPI_RESIDUAL without residual");
   if (rows < 0 || rows > (1 << 24)) return fail(WQ4_ESHAPE, "bad row count");
   if (rows == 0) return WQ4_OK;
+  if (!x || !y) return fail(WQ4_EINVAL, "null activation / output pointer");
+  if ((flags & WQ4_EPI_RESIDUAL) && !residual) return fail(WQ4_EINVAL, "WQ4_EPI_RESIDUAL without residual");
   const int ns = ns_of(prec);
   const size_t n1 = wq4::atiled_bytes(rows, fc1->g.k, ns);
   const size_t n2 = wq4::atiled_bytes(rows, fc2->g.k, ns);
@@ -332,18 +377,17 @@ static wq4_status ffn_impl(const wq4_tensor* fc1, const float* b1, const wq4_ten
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto* a1 = static_cast<_Float16*>(ws);
   auto* a2 = reinterpret_cast<_Float16*>(static_cast<uint8_t*>(ws) + n1);
-  const bool dec = use_decode(rows);
   hipError_t e = wq4::launch_tile_activations(x, a1, (int)rows, (int)fc1->g.k, (int)fc1->g.k, ns, st);
   if (e != hipSuccess) return hip_fail(e, "tile_activations launch");
   // fc1 + bias + GELU, written straight into fc2's operand layout.
   wq4::EpiArgs e1 = make_epi(b1, nullptr, nullptr, (int)fc1->g.n, (int)rows, (int)fc1->g.n, true);
   e1.out_tiled = a2;
   e1.nbp_next = (int)fc2->g.nbp;
-  e = wq4::launch_q4_gemm(fc1->g, fc1->nib, fc1->sc, a1, (int)rows, e1, wq4::kEpiTiled, ns, dec, st);
+  e = gemm(fc1, a1, rows, e1, wq4::kEpiTiled, ns, st);
   if (e != hipSuccess) return hip_fail(e, "fc1 launch");
   wq4::EpiArgs e2 = make_epi(b2, (flags & WQ4_EPI_RESIDUAL) ? residual : nullptr, y, (int)fc2->g.n, (int)rows,
                              (int)fc2->g.n, (flags & WQ4_EPI_GELU) != 0);
-  e = wq4::launch_q4_gemm(fc2->g, fc2->nib, fc2->sc, a2, (int)rows, e2, wq4::kEpiF32, ns, dec, st);
+  e = gemm(fc2, a2, rows, e2, wq4::kEpiF32, ns, st);
   if (e != hipSuccess) return hip_fail(e, "fc2 launch");
   return WQ4_OK;
 }
@@ -356,6 +400,27 @@ wq4_status wq4_ffn_forward_ws(const wq4_tensor* fc1, const float* b1_dev, const 
                   stream);
 }
 
+// Q4FFN::forward, src/model/layers.rs:54-58.
+wq4_status wq4_ffn_forward(const wq4_tensor* fc1, const float* b1_dev, const wq4_tensor* fc2,
+                           const float* b2_dev, const float* x_dev, float* y_dev, int64_t b, int64_t m,
+                           void* stream) {
+  wq4_status s = check_gemm_tensor(fc1);
+  if (s == WQ4_OK) s = check_gemm_tensor(fc2);
+  if (s != WQ4_OK) return s;
+  if (b < 0 || m < 0) return fail(WQ4_ESHAPE, "negative B or M");
+  const int64_t rows = b * m;
+  const wq4_precision prec = wq4_get_precision();
+  const int ns = ns_of(prec);
+  const size_t need = wq4::atiled_bytes(rows, fc1->g.k, ns) + wq4::atiled_bytes(rows, fc2->g.k, ns);
+  void* ws = nullptr;
+  if (rows > 0) {
+    DeviceGuard dg(fc1->device);
+    s = arena_get(fc1->device, stream, need, &ws);
+    if (s != WQ4_OK) return s;
+  }
+  return ffn_impl(fc1, b1_dev, fc2, b2_dev, x_dev, nullptr, y_dev, rows, 0u, prec, ws, need, stream);
+}
+
 size_t wq4_atiled_bytes(int64_t rows, int64_t k, wq4_precision prec) {
   if (rows < 0 || k <= 0 || k % 32 != 0) return 0;
   return wq4::atiled_bytes(rows, k, ns_of(prec));
@@ -365,9 +430,8 @@ wq4_status wq4_tile_activations(const float* x_dev, int64_t rows, int64_t k, int
                                 void* at_dev, size_t at_bytes, void* stream) {
   wq4_status s = check_prec(prec);
   if (s != WQ4_OK) return s;
+  if (rows < 0 || rows > (1 << 24) || k <= 0 || k % 32 != 0 || ld < k) return fail(WQ4_ESHAPE, "bad activation shape");
   if (!x_dev || !at_dev) return fail(WQ4_EINVAL, "null argument");
-  if (rows < 0 || rows > (1 << 24) || k <= 0 || k % 32 != 0 || ld < k)
-    return fail(WQ4_ESHAPE, "bad activation shape");
   if (at_bytes < wq4::atiled_bytes(rows, k, ns_of(prec))) return fail(WQ4_ENOMEM, "A-tiled buffer too small");
   hipError_t e = wq4::launch_tile_activations(x_dev, static_cast<_Float16*>(at_dev), (int)rows, (int)k, (int)ld,
                                               ns_of(prec), static_cast<hipStream_t>(stream));
@@ -378,17 +442,19 @@ wq4_status wq4_tile_activations(const float* x_dev, int64_t rows, int64_t k, int
 wq4_status wq4_linear_forward_tiled(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
                                     const float* residual_dev, float* y_dev, int64_t rows, unsigned flags,
                                     wq4_precision prec, void* stream) {
-  if (!w || !at_dev || !y_dev) return fail(WQ4_EINVAL, "null argument");
-  wq4_status s = check_prec(prec);
+  wq4_status s = check_gemm_tensor(w);
   if (s != WQ4_OK) return s;
-  if ((flags & WQ4_EPI_RESIDUAL) && !residual_dev) return fail(WQ4_EINVAL, "WQ4_EPI_RESIDUAL without residual");
+  s = check_prec(prec);
+  if (s != WQ4_OK) return s;
   if (rows < 0 || rows > (1 << 24)) return fail(WQ4_ESHAPE, "bad row count");
   if (rows == 0) return WQ4_OK;
+  if (!at_dev || !y_dev) return fail(WQ4_EINVAL, "null argument");
+  if ((flags & WQ4_EPI_RESIDUAL) && !residual_dev) return fail(WQ4_EINVAL, "WQ4_EPI_RESIDUAL without residual");
   DeviceGuard dg(w->device);
   wq4::EpiArgs epi = make_epi(bias_dev, (flags & WQ4_EPI_RESIDUAL) ? residual_dev : nullptr, y_dev, (int)w->g.n,
                               (int)rows, (int)w->g.n, (flags & WQ4_EPI_GELU) != 0);
-  hipError_t e = wq4::launch_q4_gemm(w->g, w->nib, w->sc, static_cast<const _Float16*>(at_dev), (int)rows, epi,
-                                     wq4::kEpiF32, ns_of(prec), use_decode(rows), static_cast<hipStream_t>(stream));
+  hipError_t e = gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, wq4::kEpiF32, ns_of(prec),
+                      static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "q4_gemm launch");
   return WQ4_OK;
 }
@@ -396,23 +462,78 @@ wq4_status wq4_linear_forward_tiled(const wq4_tensor* w, const float* bias_dev, 
 wq4_status wq4_linear_forward_tiled_out(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
                                         void* at_out_dev, size_t at_out_bytes, int64_t rows, unsigned flags,
                                         wq4_precision prec, void* stream) {
-  if (!w || !at_dev || !at_out_dev) return fail(WQ4_EINVAL, "null argument");
-  wq4_status s = check_prec(prec);
+  wq4_status s = check_gemm_tensor(w);
+  if (s != WQ4_OK) return s;
+  s = check_prec(prec);
   if (s != WQ4_OK) return s;
   if (flags & WQ4_EPI_RESIDUAL) return fail(WQ4_EUNSUPPORTED, "residual with a tiled output");
   if (rows < 0 || rows > (1 << 24)) return fail(WQ4_ESHAPE, "bad row count");
   if (w->g.n % 32 != 0) return fail(WQ4_ESHAPE, "tiled output needs N % 32 == 0");
+  if (rows == 0) return WQ4_OK;
+  if (!at_dev || !at_out_dev) return fail(WQ4_EINVAL, "null argument");
   if (at_out_bytes < wq4::atiled_bytes(rows, w->g.n, ns_of(prec)))
     return fail(WQ4_ENOMEM, "A-tiled output buffer too small");
-  if (rows == 0) return WQ4_OK;
   DeviceGuard dg(w->device);
   wq4::EpiArgs epi = make_epi(bias_dev, nullptr, nullptr, (int)w->g.n, (int)rows, (int)w->g.n,
                               (flags & WQ4_EPI_GELU) != 0);
   epi.out_tiled = static_cast<_Float16*>(at_out_dev);
   epi.nbp_next = (int)((w->g.n / 32 + 1) / 2);
-  hipError_t e = wq4::launch_q4_gemm(w->g, w->nib, w->sc, static_cast<const _Float16*>(at_dev), (int)rows, epi,
-                                     wq4::kEpiTiled, ns_of(prec), use_decode(rows), static_cast<hipStream_t>(stream));
+  hipError_t e = gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, wq4::kEpiTiled, ns_of(prec),
+                      static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "q4_gemm launch");
+  return WQ4_OK;
+}
+
+wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void* at_dev, const float* residual_dev,
+                          float* y_dev, void* at_out_dev, int64_t rows, unsigned flags, wq4_precision prec,
+                          int kernel, void* stream) {
+  wq4_status s = check_gemm_tensor(w);
+  if (s != WQ4_OK) return s;
+  s = check_prec(prec);
+  if (s != WQ4_OK) return s;
+  if (kernel < 0 || kernel > 2) return fail(WQ4_EINVAL, "kernel must be 0, 1 or 2");
+  if (rows < 0 || rows > (1 << 24)) return fail(WQ4_ESHAPE, "bad row count");
+  if (rows == 0) return WQ4_OK;
+  const bool tiled_out = (flags & WQ4_EPI_TILED_OUT) != 0;
+  if (!at_dev || (tiled_out ? !at_out_dev : !y_dev)) return fail(WQ4_EINVAL, "null argument");
+  if ((flags & WQ4_EPI_RESIDUAL) && (!residual_dev || tiled_out))
+    return fail(WQ4_EINVAL, "WQ4_EPI_RESIDUAL needs a residual and an f32 output");
+  if (tiled_out && w->g.n % 32 != 0) return fail(WQ4_ESHAPE, "tiled output needs N % 32 == 0");
+  DeviceGuard dg(w->device);
+  wq4::EpiArgs epi = make_epi(bias_dev, (flags & WQ4_EPI_RESIDUAL) ? residual_dev : nullptr, y_dev, (int)w->g.n,
+                              (int)rows, (int)w->g.n, (flags & WQ4_EPI_GELU) != 0);
+  if (tiled_out) {
+    epi.out_tiled = static_cast<_Float16*>(at_out_dev);
+    epi.nbp_next = (int)((w->g.n / 32 + 1) / 2);
+  }
+  const bool dec = kernel == 0 ? use_decode(rows) : kernel == 2;
+  hipError_t e = wq4::launch_q4_gemm(w->g, w->nib, w->sc, w->cs, static_cast<const _Float16*>(at_dev), (int)rows,
+                                     epi, tiled_out ? wq4::kEpiTiled : wq4::kEpiF32, ns_of(prec), dec,
+                                     static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "q4_gemm launch");
+  return WQ4_OK;
+}
+
+// scripts/convert_whisper.py:33-74 (numpy 2 scalar semantics: amax, d in f32).
+wq4_status wq4_quantize_q4_0(const float* x, int64_t n, uint8_t* out) {
+  if (!x || !out) return fail(WQ4_EINVAL, "null argument");
+  if (n < 0 || n % 32 != 0) return fail(WQ4_ESHAPE, "Element count " + std::to_string(n) + " not divisible by 32");
+  for (int64_t b = 0; b < n / 32; ++b) {
+    const float* blk = x + b * 32;
+    float amax = 0.0f;
+    for (int i = 0; i < 32; ++i) {
+      const float a = std::fabs(blk[i]);
+      if (a > amax || std::isnan(a)) amax = a;
+    }
+    const float d = amax > 0.0f ? amax / 7.0f : 0.0f;
+    const uint16_t h = __builtin_bit_cast(uint16_t, (_Float16)d);
+    uint8_t* o = out + b * 18;
+    o[0] = (uint8_t)(h & 0xff);
+    o[1] = (uint8_t)(h >> 8);
+    int q[32];
+    for (int i = 0; i < 32; ++i) q[i] = d > 0.0f ? (int)(int8_t)(int)std::nearbyint(blk[i] / d) : 0;
+    for (int i = 0; i < 16; ++i) o[2 + i] = (uint8_t)(((q[i] + 8) & 0x0f) | (((q[i + 16] + 8) & 0x0f) << 4));
+  }
   return WQ4_OK;
 }
 
@@ -422,49 +543,33 @@ static wq4_status check_nk(int64_t n, int64_t k) {
   return WQ4_OK;
 }
 
-wq4_status wq4_debug_repacked_bytes(int64_t n, int64_t k, size_t* nib_bytes, size_t* sc_bytes) {
+wq4_status wq4_debug_repacked_bytes(int64_t n, int64_t k, size_t* nib_bytes, size_t* sc_bytes, size_t* cs_bytes) {
   wq4_status s = check_nk(n, k);
   if (s != WQ4_OK) return s;
-  if (!nib_bytes || !sc_bytes) return fail(WQ4_EINVAL, "null argument");
+  if (!nib_bytes || !sc_bytes || !cs_bytes) return fail(WQ4_EINVAL, "null argument");
   const wq4::Q4Geom g = wq4::make_geom(n, k);
   *nib_bytes = g.nib_bytes();
   *sc_bytes = g.sc_bytes();
+  *cs_bytes = g.colscale_bytes();
   return WQ4_OK;
 }
 
-wq4_status wq4_debug_repack(const uint8_t* raw, int64_t n, int64_t k, uint8_t* nib_out, uint32_t* sc_out) {
+wq4_status wq4_debug_repack(const uint8_t* raw, int64_t n, int64_t k, uint8_t* nib_out, uint32_t* sc_out,
+                            float* colscale_out) {
   wq4_status s = check_nk(n, k);
   if (s != WQ4_OK) return s;
-  if (!raw || !nib_out || !sc_out) return fail(WQ4_EINVAL, "null argument");
-  wq4::repack_q4(raw, wq4::make_geom(n, k), nib_out, sc_out);
+  if (!raw || !nib_out || !sc_out || !colscale_out) return fail(WQ4_EINVAL, "null argument");
+  wq4::repack_q4(raw, wq4::make_geom(n, k), nib_out, sc_out, colscale_out);
   return WQ4_OK;
 }
 
-wq4_status wq4_debug_unrepack(const uint8_t* nib, const uint32_t* sc, int64_t n, int64_t k, uint8_t* raw_out) {
+wq4_status wq4_debug_unrepack(const uint8_t* nib, const uint32_t* sc, const float* colscale, int64_t n, int64_t k,
+                              uint8_t* raw_out) {
   wq4_status s = check_nk(n, k);
   if (s != WQ4_OK) return s;
-  if (!nib || !sc || !raw_out) return fail(WQ4_EINVAL, "null argument");
-  wq4::unrepack_q4(nib, sc, wq4::make_geom(n, k), raw_out);
+  if (!nib || !sc || !colscale || !raw_out) return fail(WQ4_EINVAL, "null argument");
+  wq4::unrepack_q4(nib, sc, colscale, wq4::make_geom(n, k), raw_out);
   return WQ4_OK;
-}
-
-// Q4FFN::forward, src/model/layers.rs:54-58.
-wq4_status wq4_ffn_forward(const wq4_tensor* fc1, const float* b1_dev, const wq4_tensor* fc2,
-                           const float* b2_dev, const float* x_dev, float* y_dev, int64_t b, int64_t m,
-                           void* stream) {
-  if (!fc1 || !fc2) return fail(WQ4_EINVAL, "weights are null");
-  if (b < 0 || m < 0) return fail(WQ4_ESHAPE, "negative B or M");
-  const int64_t rows = b * m;
-  const wq4_precision prec = wq4_get_precision();
-  const int ns = ns_of(prec);
-  const size_t need = wq4::atiled_bytes(rows, fc1->g.k, ns) + wq4::atiled_bytes(rows, fc2->g.k, ns);
-  void* ws = nullptr;
-  {
-    DeviceGuard dg(fc1->device);
-    wq4_status s = arena_get(fc1->device, stream, need, &ws);
-    if (s != WQ4_OK) return s;
-  }
-  return ffn_impl(fc1, b1_dev, fc2, b2_dev, x_dev, nullptr, y_dev, rows, 0u, prec, ws, need, stream);
 }
 
 }  // extern "C"

@@ -13,8 +13,6 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-
-
 // tanh-approximate GELU, src/model/layers.rs:35-41.
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float s = 0.7978845608028654f;  // sqrt(2/pi)
@@ -31,8 +29,8 @@ __device__ __forceinline__ float epi_value(float acc, int row, int col, const Ep
   return v;
 }
 
-// One repacked u32 (8 nibbles, see wq4_layout.hpp) -> MFMA B operand of 8
-// exact f16 values (q - 8), element order j = 0..7.
+// One repacked u32 (8 nibbles, see wq4_layout.hpp) -> 8 exact f16 (q - 8),
+// element order j = 0..7:
 //   (w & 0x000F000F) | 0x64006400 = f16 pair (1024 + q_a, 1024 + q_b)
 //   (w & 0x00F000F0) | 0x64006400 = f16 pair (1024 + 16 q_a, ...)
 // then -1032 resp. *(1/16) - 72; every step is exact in f16.
@@ -58,8 +56,15 @@ __device__ __forceinline__ half8 deq8(uint32_t w) {
   return r;
 }
 
-__device__ __forceinline__ float f16bits_to_f32(uint32_t bits16) {
-  return (float)__builtin_bit_cast(_Float16, (uint16_t)bits16);
+// MFMA B operand for one k-half: B = (q - 8) * d' as the exact f16 pair
+// hi = RN(B), lo = B - hi (the fma is exact: B has <= 14 significant bits).
+template <int NB>
+__device__ __forceinline__ void deq_scaled(uint32_t w, uint32_t dbits, half8& hi, half8& lo) {
+  const half8 q = deq8(w);
+  const _Float16 d = __builtin_bit_cast(_Float16, (uint16_t)dbits);
+  const half8 dv = {d, d, d, d, d, d, d, d};
+  hi = q * dv;
+  if constexpr (NB == 2) lo = __builtin_elementwise_fma(q, dv, -hi);
 }
 
 __device__ __forceinline__ floatx16 mfma32(const half8& a, const half8& b, const floatx16& c) {
@@ -79,6 +84,13 @@ __device__ __forceinline__ int xcd_remap(int L, int nwg) {
   const int q = nwg / 8, r = nwg % 8;
   const int xcd = L % 8, idx = L / 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+// Async 16-B-per-lane global -> LDS copy (global_load_lds_dwordx4): lane l's
+// 16 bytes land at lds_base + 16 * l (lds_base wave-uniform).
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
 }  // namespace wq4

@@ -2,9 +2,14 @@
 // and its exact inverse.  Layout spec: wq4_layout.hpp.
 #include "wq4_layout.hpp"
 
+#include <cmath>
 #include <cstring>
+#include <vector>
 
 namespace wq4 {
+
+static inline float h2f(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
+static inline uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
 
 static inline uint32_t pack_half(const uint8_t* bytes, int kk) {
   // bytes -> 8 raw nibble bytes (8h..8h+7 of one block); kk selects the
@@ -32,17 +37,44 @@ static inline void unpack_half(uint32_t w, int kk, uint8_t* bytes) {
   }
 }
 
-void repack_q4(const uint8_t* raw, const Q4Geom& g, uint8_t* nib, uint32_t* sc) {
+// Exponent shift s for one output row: 8 * max d' <= 2^15, every nonzero
+// d * 2^s still an exact f16 (else 0, i.e. no shift).
+static int row_shift(const uint8_t* row, int64_t kb) {
+  float dmax = 0.0f;
+  for (int64_t b = 0; b < kb; ++b) {
+    const float d = std::fabs(h2f((uint16_t)(row[b * kBlockBytes] | (row[b * kBlockBytes + 1] << 8))));
+    if (!std::isfinite(d)) return 0;
+    dmax = d > dmax ? d : dmax;
+  }
+  if (dmax == 0.0f) return 0;
+  const int s = (int)std::floor(std::log2(4096.0 / (double)dmax));  // dmax * 2^s in (2^11, 2^12]
+  for (int64_t b = 0; b < kb; ++b) {
+    const uint16_t bits = (uint16_t)(row[b * kBlockBytes] | (row[b * kBlockBytes + 1] << 8));
+    const float d = h2f(bits);
+    const float ds = std::ldexp(d, s);
+    if (std::fabs(ds) > 4096.0f) return 0;
+    const uint16_t hb = f2h(ds);
+    if (std::ldexp(h2f(hb), -s) != d || f2h(std::ldexp(h2f(hb), -s)) != bits) return 0;
+  }
+  return s;
+}
+
+void repack_q4(const uint8_t* raw, const Q4Geom& g, uint8_t* nib, uint32_t* sc, float* colscale) {
   std::memset(nib, 0, g.nib_bytes());
   std::memset(sc, 0, g.sc_bytes());
+  for (int64_t n = 0; n < g.np; ++n) colscale[n] = 1.0f;
   for (int64_t n = 0; n < g.n; ++n) {
     const int64_t nt = n / kNTile, r = n % kNTile;
+    const uint8_t* row = raw + n * g.kb * kBlockBytes;
+    const int s = row_shift(row, g.kb);
+    colscale[n] = std::ldexp(1.0f, -s);
     for (int64_t b = 0; b < g.kb; ++b) {
-      const uint8_t* blk = raw + (n * g.kb + b) * kBlockBytes;
+      const uint8_t* blk = row + b * kBlockBytes;
       const int64_t bp = b / 2, bi = b % 2;
-      const uint32_t d = (uint32_t)blk[0] | ((uint32_t)blk[1] << 8);
-      uint32_t& s = sc[(nt * g.nbp + bp) * 32 + r];
-      s |= d << (16 * bi);
+      const uint16_t dbits = (uint16_t)(blk[0] | (blk[1] << 8));
+      const uint32_t d = s ? f2h(std::ldexp(h2f(dbits), s)) : dbits;
+      uint32_t& w = sc[(nt * g.nbp + bp) * 32 + r];
+      w |= d << (16 * bi);
       for (int h = 0; h < 2; ++h) {
         const int lane = (int)r + 32 * h;
         uint32_t* dst = reinterpret_cast<uint32_t*>(nib + ((nt * g.nbp + bp) * 64 + lane) * 16);
@@ -52,13 +84,15 @@ void repack_q4(const uint8_t* raw, const Q4Geom& g, uint8_t* nib, uint32_t* sc) 
   }
 }
 
-void unrepack_q4(const uint8_t* nib, const uint32_t* sc, const Q4Geom& g, uint8_t* raw) {
+void unrepack_q4(const uint8_t* nib, const uint32_t* sc, const float* colscale, const Q4Geom& g, uint8_t* raw) {
   for (int64_t n = 0; n < g.n; ++n) {
     const int64_t nt = n / kNTile, r = n % kNTile;
+    const int s = -(int)std::lround(std::log2((double)colscale[n]));
     for (int64_t b = 0; b < g.kb; ++b) {
       uint8_t* blk = raw + (n * g.kb + b) * kBlockBytes;
       const int64_t bp = b / 2, bi = b % 2;
-      const uint32_t d = (sc[(nt * g.nbp + bp) * 32 + r] >> (16 * bi)) & 0xffffu;
+      const uint16_t ds = (uint16_t)((sc[(nt * g.nbp + bp) * 32 + r] >> (16 * bi)) & 0xffffu);
+      const uint16_t d = s ? f2h(std::ldexp(h2f(ds), -s)) : ds;
       blk[0] = (uint8_t)(d & 0xff);
       blk[1] = (uint8_t)(d >> 8);
       for (int h = 0; h < 2; ++h) {

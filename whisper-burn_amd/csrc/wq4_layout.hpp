@@ -16,7 +16,15 @@
 //     w = sum_i q[j=2i] << 4i | q[j=2i+1] << (16+4i),  i = 0..3
 //   which turns into the MFMA B operand (8 x f16 (q-8), order j) with
 //   4 v_and_or + 1 shift + 4 packed-f16 ops (wq4_device.hpp deq8()).
-//   sc[nt][bp][32 n] : u32 = { f16 d(blk 2bp), f16 d(blk 2bp+1) }
+//   sc[nt][bp][32 n] : u32 = { f16 d'(blk 2bp), f16 d'(blk 2bp+1) }
+//   colscale[n]      : f32 2^-s_n
+// where d' = d * 2^s_n exactly (a pure exponent shift of the GGUF f16 scale)
+// and s_n is chosen per output row so that 8 * max_b d'_{n,b} <= 2^15: the
+// kernels build the MFMA B operand as the exact two-term f16 sum
+//   B_hi + B_lo = (q - 8) * d'      (B_hi = f16 RN, B_lo = f16 remainder)
+// and multiply each output column by colscale once, in the epilogue.  If a
+// row's scales span more than the f16 range allows (d_max/d_min > 2^26) its
+// s_n is 0 and d' = d.  The repack stays lossless (unrepack_q4 recovers d).
 //
 // N is padded to a multiple of 64 and the block count to a multiple of 2 with
 // d = 0 blocks (they contribute exactly 0).
@@ -39,7 +47,7 @@ constexpr int kBlockBytes = 18;  // f16 scale + 16 nibble bytes
 constexpr int kNTile = 32;       // output rows per MFMA n-tile
 constexpr int kNPad = 64;        // N padding granule
 constexpr int kMTile = 32;       // activation rows per m-tile
-constexpr int kMPad = 64;        // M padding granule of A-tiled buffers
+constexpr int kMPad = 128;       // M padding granule of A-tiled buffers
 
 struct Q4Geom {
   int64_t n = 0, k = 0;   // logical [N, K]
@@ -49,6 +57,7 @@ struct Q4Geom {
   int64_t ntiles = 0;     // np / 32
   size_t nib_bytes() const { return (size_t)ntiles * nbp * 1024; }
   size_t sc_bytes() const { return (size_t)ntiles * nbp * 32 * 4; }
+  size_t colscale_bytes() const { return (size_t)np * 4; }
 };
 
 inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
@@ -72,8 +81,8 @@ inline size_t atiled_bytes(int64_t rows, int64_t k, int ns) {
 }
 
 // Host-side repack of raw GGUF Q4_0 bytes into nib/sc (see header comment).
-void repack_q4(const uint8_t* raw, const Q4Geom& g, uint8_t* nib, uint32_t* sc);
+void repack_q4(const uint8_t* raw, const Q4Geom& g, uint8_t* nib, uint32_t* sc, float* colscale);
 // Exact inverse (for Q4Tensor::dequantize and the lossless check).
-void unrepack_q4(const uint8_t* nib, const uint32_t* sc, const Q4Geom& g, uint8_t* raw);
+void unrepack_q4(const uint8_t* nib, const uint32_t* sc, const float* colscale, const Q4Geom& g, uint8_t* raw);
 
 }  // namespace wq4

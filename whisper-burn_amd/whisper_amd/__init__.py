@@ -1,0 +1,155 @@
+"""whisper_amd -- Python binding of the Whisper model runtime (include/whisper_amd.h).
+
+Mirrors WhisperModel::{new, encode, transcribe} (zerr0o/whisper-burn
+src/model/whisper.rs) over lib/libwhisper_amd.so; every Q4 projection runs in
+lib/libwq4.so.  Loud failure if the native libraries are missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+import wq4
+
+LIB_PATH = os.path.join(os.path.dirname(wq4.LIB_PATH), "libwhisper_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(wq4.HEADER_PATH), "whisper_amd.h")
+VARIANTS = {"large_v3": 0, "medium": 1, "tiny_test": 2}
+CFG_KEYS = ["n_mels", "n_audio_ctx", "n_audio_state", "n_audio_head", "n_audio_layer", "n_text_ctx",
+            "n_text_state", "n_text_head", "n_text_layer", "n_vocab", "n_lang"]
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        wq4.lib()  # libwq4.so first (RTLD_GLOBAL)
+        if not os.path.exists(LIB_PATH):
+            raise wq4.WQ4Error(6, f"{LIB_PATH} not built")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        vp, c_int, c_i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        f32p = ctypes.POINTER(ctypes.c_float)
+        L.wa_last_error.restype = ctypes.c_char_p
+        L.wa_model_create_synthetic.argtypes = [c_int, c_int, ctypes.c_uint64, c_int, c_int, ctypes.POINTER(vp)]
+        L.wa_model_destroy.argtypes = [vp]
+        L.wa_model_destroy.restype = None
+        L.wa_model_config.argtypes = [vp, i32p]
+        L.wa_model_device_bytes.argtypes = [vp]
+        L.wa_model_device_bytes.restype = ctypes.c_size_t
+        L.wa_transcribe.argtypes = [vp, vp, c_int, c_int, c_int, c_int, i32p, i32p, vp]
+        L.wa_last_timings.argtypes = [vp, f32p]
+        L.wa_encode.argtypes = [vp, vp, c_int, vp, vp]
+        L.wa_prompt_logits.argtypes = [vp, vp, c_int, c_int, vp, vp]
+        L.wa_synth_uniform.argtypes = [ctypes.c_uint64, ctypes.c_char_p, c_i64, ctypes.c_float, ctypes.c_float, f32p]
+        L.wa_profile_enable.argtypes = [vp, c_int]
+        L.wa_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), c_int]
+        for n in ("wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
+                  "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read"):
+            getattr(L, n).restype = c_int
+        _lib = L
+    return _lib
+
+
+def check(st: int) -> None:
+    if st != 0:
+        raise wq4.WQ4Error(st, lib().wa_last_error().decode(errors="replace"))
+
+
+def synth_uniform(seed: int, name: str, n: int, lo: float, hi: float) -> np.ndarray:
+    out = np.empty(n, np.float32)
+    check(lib().wa_synth_uniform(seed, name.encode(), n, lo, hi, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+    return out
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+class WhisperModel:
+    """A Whisper model with synthetic weights resident on one MI355X."""
+
+    def __init__(self, variant: str = "large_v3", seed: int = 1234, max_batch: int = 1, device: int = 0,
+                 precision: int = wq4.PREC_F16X2):
+        h = ctypes.c_void_p(None)
+        check(lib().wa_model_create_synthetic(device, VARIANTS[variant], seed, max_batch, precision,
+                                              ctypes.byref(h)))
+        self._h = h
+        self.device = device
+        self.variant = variant
+        self.max_batch = max_batch
+        cfg = (ctypes.c_int32 * len(CFG_KEYS))()
+        check(lib().wa_model_config(h, cfg))
+        self.config = dict(zip(CFG_KEYS, list(cfg)))
+
+    def device_bytes(self) -> int:
+        return int(lib().wa_model_device_bytes(self._h))
+
+    def _stream(self):
+        return ctypes.c_void_p(_torch().cuda.current_stream(self.device).cuda_stream)
+
+    def transcribe(self, mel, lang_token: Optional[int] = 50259, max_tokens: int = 224, eot_stop: bool = True):
+        """whisper.rs:51-128 for a batch of clips; mel: cuda f32 [B, n_mels, 3000].
+        Returns a list of token-id lists (special tokens excluded)."""
+        torch = _torch()
+        mel = mel.contiguous()
+        assert mel.dtype == torch.float32 and mel.is_cuda
+        B = mel.shape[0]
+        toks = np.zeros((B, max_tokens), np.int32)
+        nt = np.zeros(B, np.int32)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        check(lib().wa_transcribe(self._h, ctypes.c_void_p(mel.data_ptr()), B,
+                                  -1 if lang_token is None else int(lang_token), max_tokens, 1 if eot_stop else 0,
+                                  toks.ctypes.data_as(i32p), nt.ctypes.data_as(i32p), self._stream()))
+        return [toks[b, : nt[b]].tolist() for b in range(B)]
+
+    def last_timings(self) -> dict:
+        t = (ctypes.c_float * 5)()
+        check(lib().wa_last_timings(self._h, t))
+        return {"encoder_ms": t[0], "cross_kv_ms": t[1], "prompt_ms": t[2], "decode_ms": t[3], "steps": int(t[4])}
+
+    PROF_NAMES = ("q4_gemm", "encoder_attention", "conv", "layernorm")
+
+    def profile_enable(self, on: bool = True) -> None:
+        check(lib().wa_profile_enable(self._h, 1 if on else 0))
+
+    def profile_read(self, reset: bool = True) -> dict:
+        """Per category: launches, ms, algorithmic GFLOP and GB (HIP events)."""
+        buf = (ctypes.c_double * 16)()
+        check(lib().wa_profile_read(self._h, buf, 1 if reset else 0))
+        return {n: {"launches": int(buf[4 * i]), "ms": buf[4 * i + 1], "gflop": buf[4 * i + 2], "gb": buf[4 * i + 3]}
+                for i, n in enumerate(self.PROF_NAMES)}
+
+    def encode(self, mel):
+        """encoder.rs:87-115 -> encoder_out [B, 1500, D] (also fills the cross-K/V caches)."""
+        torch = _torch()
+        B = mel.shape[0]
+        out = torch.empty((B, self.config["n_audio_ctx"], self.config["n_audio_state"]), device=mel.device,
+                          dtype=torch.float32)
+        check(lib().wa_encode(self._h, ctypes.c_void_p(mel.contiguous().data_ptr()), B,
+                              ctypes.c_void_p(out.data_ptr()), self._stream()))
+        return out
+
+    def prompt_logits(self, prompt):
+        """decoder.rs:251-296 after encode(): prompt int32 cuda [B, T<=4] -> last-position logits."""
+        torch = _torch()
+        B, T = prompt.shape
+        out = torch.empty((B, self.config["n_vocab"]), device=prompt.device, dtype=torch.float32)
+        check(lib().wa_prompt_logits(self._h, ctypes.c_void_p(prompt.contiguous().data_ptr()), B, T,
+                                     ctypes.c_void_p(out.data_ptr()), self._stream()))
+        return out
+
+    def close(self):
+        if self._h and self._h.value:
+            lib().wa_model_destroy(self._h)
+            self._h = ctypes.c_void_p(None)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

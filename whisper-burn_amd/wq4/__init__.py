@@ -72,9 +72,10 @@ def _declare(L: ctypes.CDLL) -> None:
     L.wq4_ffn_workspace_bytes.restype = c_sz
     L.wq4_linear_forward_ws.argtypes = [vp, vp, vp, vp, vp, c_i64, c_i64, ctypes.c_uint, c_int, vp, c_sz, vp]
     L.wq4_ffn_forward_ws.argtypes = [vp, vp, vp, vp, vp, vp, vp, c_i64, ctypes.c_uint, c_int, vp, c_sz, vp]
-    L.wq4_debug_repack.argtypes = [u8p, c_i64, c_i64, u8p, ctypes.POINTER(ctypes.c_uint32)]
-    L.wq4_debug_unrepack.argtypes = [u8p, ctypes.POINTER(ctypes.c_uint32), c_i64, c_i64, u8p]
-    L.wq4_debug_repacked_bytes.argtypes = [c_i64, c_i64, ctypes.POINTER(c_sz), ctypes.POINTER(c_sz)]
+    L.wq4_debug_repack.argtypes = [u8p, c_i64, c_i64, u8p, ctypes.POINTER(ctypes.c_uint32), f32p]
+    L.wq4_debug_unrepack.argtypes = [u8p, ctypes.POINTER(ctypes.c_uint32), f32p, c_i64, c_i64, u8p]
+    L.wq4_debug_repacked_bytes.argtypes = [c_i64, c_i64, ctypes.POINTER(c_sz), ctypes.POINTER(c_sz),
+                                           ctypes.POINTER(c_sz)]
     L.wq4_atiled_bytes.argtypes = [c_i64, c_i64, c_int]
     L.wq4_atiled_bytes.restype = c_sz
     L.wq4_tile_activations.argtypes = [vp, c_i64, c_i64, c_i64, c_int, vp, c_sz, vp]
@@ -136,22 +137,29 @@ def _u8p(a: np.ndarray):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
 
 
-def debug_repack(raw: np.ndarray, n: int, k: int) -> tuple[np.ndarray, np.ndarray]:
-    """Host-only: the upload repack (wq4_layout.cpp) without touching a GPU."""
-    nb, sb = ctypes.c_size_t(0), ctypes.c_size_t(0)
-    check(lib().wq4_debug_repacked_bytes(n, k, ctypes.byref(nb), ctypes.byref(sb)))
+def _f32p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def debug_repack(raw: np.ndarray, n: int, k: int) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Host-only: the upload repack (wq4_layout.cpp) without touching a GPU.
+    Returns (nibbles u8, scales u32 = 2 x f16 d', column scales f32)."""
+    nb, sb, cb = ctypes.c_size_t(0), ctypes.c_size_t(0), ctypes.c_size_t(0)
+    check(lib().wq4_debug_repacked_bytes(n, k, ctypes.byref(nb), ctypes.byref(sb), ctypes.byref(cb)))
     raw = np.ascontiguousarray(raw, np.uint8)
     nib = np.zeros(nb.value, np.uint8)
     sc = np.zeros(sb.value // 4, np.uint32)
-    check(lib().wq4_debug_repack(_u8p(raw), n, k, _u8p(nib), sc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
-    return nib, sc
+    cs = np.zeros(cb.value // 4, np.float32)
+    check(lib().wq4_debug_repack(_u8p(raw), n, k, _u8p(nib), sc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                 _f32p(cs)))
+    return nib, sc, cs
 
 
-def debug_unrepack(nib: np.ndarray, sc: np.ndarray, n: int, k: int) -> np.ndarray:
+def debug_unrepack(nib: np.ndarray, sc: np.ndarray, cs: np.ndarray, n: int, k: int) -> np.ndarray:
     out = np.zeros(n * k // 32 * 18, np.uint8)
     check(lib().wq4_debug_unrepack(_u8p(np.ascontiguousarray(nib, np.uint8)),
                                    np.ascontiguousarray(sc, np.uint32).ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
-                                   n, k, _u8p(out)))
+                                   _f32p(np.ascontiguousarray(cs, np.float32)), n, k, _u8p(out)))
     return out
 
 
