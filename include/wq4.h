@@ -152,6 +152,16 @@ wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void
                           float* y_dev, void* at_out_dev, int64_t rows, unsigned flags, wq4_precision prec,
                           int kernel, void* stream);
 
+/* Fused K|V projection written head-major for attention: w is [parts * d, K]
+ * (parts stacked projections of d = heads * 64 columns each), rows =
+ * groups * group_rows; y_dev[part][group][head][t][64] (the [B, H, T, 64]
+ * view of the cross-attention k / v after reshape + swap_dims(1, 2),
+ * zerr0o/whisper-burn src/model/attention.rs:177-206, 254-263).
+ * d % 64 == 0.                                                          */
+wq4_status wq4_gemm_tiled_headmajor(const wq4_tensor* w, const float* bias_dev, const void* at_dev, float* y_dev,
+                                    int64_t rows, int group_rows, int d, wq4_precision prec, int kernel,
+                                    void* stream);
+
 /* ---- conversion (scripts/convert_whisper.py:33-74) -------------------- */
 /* Q4_0-quantize n f32 values (n % 32 == 0) exactly as the reference's
  * converter does under numpy 2: d = amax/7 (f32), f16 scale, round-half-even

@@ -349,3 +349,34 @@ def test_linear_ws_residual_and_gelu(torch):
     h = x.cpu().numpy().astype(np.float64) @ deq.T.astype(np.float64) + b.cpu().numpy()
     want = res.cpu().numpy() + oracle.gelu_np(h.astype(np.float32))
     assert np.max(np.abs(y.cpu().numpy() - want)) < 1e-4
+
+
+@pytest.mark.parametrize("policy", [1, 2])
+def test_gemm_headmajor_layout(torch, policy):
+    """wq4_gemm_tiled_headmajor == row-major GEMM permuted to [part][g][head][t][64]."""
+    import ctypes
+
+    d, k, groups, trows = 128, 256, 2, 24  # parts = 2 (K | V), heads of 64
+    n, m = 2 * d, groups * trows
+    rng = np.random.default_rng(21)
+    q = oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.05).astype(np.float32))
+    t = wq4.Q4Tensor.from_q4_bytes(q, [n, k])
+    x = to_dev(torch, rng.standard_normal(m * k).astype(np.float32), (m, k))
+    b = to_dev(torch, (rng.standard_normal(n) * 0.1).astype(np.float32), (n,))
+    L = wq4.lib()
+    atb = L.wq4_atiled_bytes(m, k, wq4.PREC_F16X2)
+    at = torch.zeros(atb, dtype=torch.uint8, device="cuda:0")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    wq4.check(L.wq4_tile_activations(ctypes.c_void_p(x.data_ptr()), m, k, k, wq4.PREC_F16X2,
+                                     ctypes.c_void_p(at.data_ptr()), atb, st))
+    ref = torch.empty((m, n), device="cuda:0", dtype=torch.float32)
+    hm = torch.empty((m * n,), device="cuda:0", dtype=torch.float32)
+    wq4.check(L.wq4_gemm_tiled(t.handle, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(at.data_ptr()), None,
+                               ctypes.c_void_p(ref.data_ptr()), None, m, 0, wq4.PREC_F16X2, policy, st))
+    wq4.check(L.wq4_gemm_tiled_headmajor(t.handle, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(at.data_ptr()),
+                                         ctypes.c_void_p(hm.data_ptr()), m, trows, d, wq4.PREC_F16X2, policy, st))
+    want = ref.cpu().numpy().reshape(groups, trows, 2, d // 64, 64).transpose(2, 0, 3, 1, 4).ravel()
+    assert np.array_equal(hm.cpu().numpy(), want)
+    with pytest.raises(wq4.WQ4Error):
+        wq4.check(L.wq4_gemm_tiled_headmajor(t.handle, None, ctypes.c_void_p(at.data_ptr()),
+                                             ctypes.c_void_p(hm.data_ptr()), m, 25, d, wq4.PREC_F16X2, policy, st))

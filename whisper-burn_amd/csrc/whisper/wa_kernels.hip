@@ -70,6 +70,9 @@ __device__ __forceinline__ void atile_store4(_Float16* t, int row, int k, int kb
 __host__ __device__ inline int kbp_of(int k) { return ((k / 32 + 1) / 2) * 2; }
 
 // ------------------------------------------------------------------ LN --
+// One wave per row; the row stays in registers (D <= 64 * 4 * kLnMaxV).
+constexpr int kLnMaxV = 8;
+
 template <int NS, bool TILED>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ bb, int M, int D,
@@ -77,41 +80,49 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kbp = kbp_of(D);
   const int rows_total = TILED ? ((M + 31) / 32) * 32 : M;
-  for (int rr = 0; rr < 8; ++rr) {
-    const int row = blockIdx.x * 32 + wave * 8 + rr;
-    if (row >= rows_total) break;
-    if (row < M) {
-      const float* xr = x + (size_t)row * D;
-      float s = 0.0f;
-      for (int k = lane * 4; k < D; k += 256) {
-        const floatx4 v = *reinterpret_cast<const floatx4*>(xr + k);
-        s += (v[0] + v[1]) + (v[2] + v[3]);
-      }
-      const float mean = wave_sum(s) / (float)D;
-      float s2 = 0.0f;
-      for (int k = lane * 4; k < D; k += 256) {
-        const floatx4 v = *reinterpret_cast<const floatx4*>(xr + k);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float c = v[j] - mean;
-          s2 += c * c;
-        }
-      }
-      const float den = sqrtf(wave_sum(s2) / (float)D + 1e-5f);
-      for (int k = lane * 4; k < D; k += 256) {
-        const floatx4 v = *reinterpret_cast<const floatx4*>(xr + k);
-        const floatx4 g = *reinterpret_cast<const floatx4*>(w + k);
-        const floatx4 be = *reinterpret_cast<const floatx4*>(bb + k);
-        float y[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) y[j] = ((v[j] - mean) / den) * g[j] + be[j];
-        if constexpr (TILED)
-          atile_store4<NS>(tiled, row, k, kbp, y[0], y[1], y[2], y[3]);
-        else
-          *reinterpret_cast<floatx4*>(out + (size_t)row * D + k) = floatx4{y[0], y[1], y[2], y[3]};
-      }
-    } else if constexpr (TILED) {
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= rows_total) return;
+  if (row >= M) {  // padded rows of the last m-tile: finite zeros
+    if constexpr (TILED)
       for (int k = lane * 4; k < D; k += 256) atile_store4<NS>(tiled, row, k, kbp, 0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  const float* xr = x + (size_t)row * D;
+  floatx4 v[kLnMaxV];
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < kLnMaxV; ++i) {
+    const int k = lane * 4 + 256 * i;
+    v[i] = k < D ? *reinterpret_cast<const floatx4*>(xr + k) : floatx4{0.f, 0.f, 0.f, 0.f};
+    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float s2 = 0.0f;
+#pragma unroll
+  for (int i = 0; i < kLnMaxV; ++i) {
+    const int k = lane * 4 + 256 * i;
+    if (k < D) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float c = v[i][j] - mean;
+        s2 += c * c;
+      }
+    }
+  }
+  const float den = sqrtf(wave_sum(s2) / (float)D + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < kLnMaxV; ++i) {
+    const int k = lane * 4 + 256 * i;
+    if (k < D) {
+      const floatx4 g = *reinterpret_cast<const floatx4*>(w + k);
+      const floatx4 be = *reinterpret_cast<const floatx4*>(bb + k);
+      float y[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[j] = ((v[i][j] - mean) / den) * g[j] + be[j];
+      if constexpr (TILED)
+        atile_store4<NS>(tiled, row, k, kbp, y[0], y[1], y[2], y[3]);
+      else
+        *reinterpret_cast<floatx4*>(out + (size_t)row * D + k) = floatx4{y[0], y[1], y[2], y[3]};
     }
   }
 }
@@ -119,7 +130,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 hipError_t launch_layernorm(const float* x, const float* w, const float* b, int M, int D, _Float16* tiled, int ns,
                             float* out, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  const dim3 grid((M + 31) / 32), block(256);
+  if (D % 4 != 0 || D > 256 * kLnMaxV) return hipErrorInvalidValue;
+  const int rows_total = tiled ? ((M + 31) / 32) * 32 : M;
+  const dim3 grid((rows_total + 3) / 4), block(256);
   if (tiled) {
     if (ns == 2)
       hipLaunchKernelGGL((layernorm_kernel<2, true>), grid, block, 0, st, x, w, b, M, D, tiled, out);
@@ -318,53 +331,76 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
 }
 
 // ------------------------------------------------- cross-attention --
-// One workgroup per (head, clip): 4 waves split the T encoder keys; inside a
-// wave 16 lanes share one key (4 dims each), 4 keys per instruction, with
-// an online softmax per 16-lane group, merged across groups and waves.
-template <int NS>
+// Memory-bound GEMV over the cross K/V cache (B * 1500 * 2D floats per
+// layer and step).  Grid = (H * S, B): the T encoder keys of each (head,
+// clip) are split over S workgroups (S depends on T only -> batch
+// invariant) so the chip sees ~10 balanced workgroups per CU instead of 2-3
+// unbalanced ones.  Inside a workgroup 4 waves split the keys; 16 lanes share
+// one key (4 dims each), 4 keys per load instruction, U instructions in
+// flight, online softmax per 16-lane group, merged across groups and waves in
+// a fixed order.  With S > 1 each workgroup publishes (m, l, o[64]) per query
+// write-through (sc1); the last arriver of the (head, clip) merges the S
+// partials in split order (cdna_hip_programming.md Guideline 16, R1) and
+// writes the A-tiled operand of the output projection.
+constexpr int kXattnMaxSplit = 8;
+constexpr int kXattnPart = 68;  // floats per (query) partial: o[64], m, l, pad
+
+int cross_attention_splits(int T) {
+  const int s = T / 375;
+  return s < 1 ? 1 : (s > kXattnMaxSplit ? kXattnMaxSplit : s);
+}
+
+template <int NS, int TQ>
 __global__ __launch_bounds__(256) void cross_attn_kernel(const float* __restrict__ q, const float* __restrict__ kv,
-                                                         int Tq, int T, int H, _Float16* __restrict__ tiled) {
-  __shared__ float wm[4][4], wl[4][4];
-  __shared__ float wo[4][4][64];
+                                                         int Tq_, int T, int H, int S, float* __restrict__ part,
+                                                         int* __restrict__ counters, _Float16* __restrict__ tiled) {
+  // TQ = 1 (decode step) keeps one query's state: ~half the VGPRs, twice the
+  // resident waves of the TQ = 4 (prompt) instance
+  const int Tq = TQ == 1 ? 1 : Tq_;
+  __shared__ float wm[4][TQ], wl[4][TQ];
+  __shared__ float wo[4][TQ][64];
+  __shared__ int last_flag;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int head = blockIdx.x, b = blockIdx.y;
+  const int head = blockIdx.x / S, split = blockIdx.x - head * S, b = blockIdx.y;
   const int D = H * 64;
   const int sub = lane & 15, grp = lane >> 4;
-  floatx4 qv[4];
+  floatx4 qv[TQ];
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+  for (int t = 0; t < TQ; ++t)
     qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(q + (size_t)(b * Tq + t) * D + head * 64 + sub * 4)
                    : floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int t = 0; t < 4; ++t) qv[t] = qv[t] * 0.125f;
-  float m[4], l[4];
-  floatx4 o[4];
+  for (int t = 0; t < TQ; ++t) qv[t] = qv[t] * 0.125f;
+  float m[TQ], l[TQ];
+  floatx4 o[TQ];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < TQ; ++t) {
     m[t] = -INFINITY;
     l[t] = 0.0f;
     o[t] = floatx4{0.f, 0.f, 0.f, 0.f};
   }
-  const int per_wave = (T + 3) / 4;
-  const int k0 = wave * per_wave, k1 = min(T, k0 + per_wave);
-  const float* kvb = kv + (size_t)b * T * 2 * D + head * 64 + sub * 4;
-  constexpr int U = 4;  // 16 keys per wave per iteration in flight
+  const int per_split = (T + S - 1) / S;
+  const int s0 = split * per_split, s1 = min(T, s0 + per_split);
+  const int per_wave = (s1 - s0 + 3) / 4;
+  const int k0 = min(s1, s0 + wave * per_wave), k1 = min(s1, k0 + per_wave);
+  // head-major K / V: [2][B][H][T][64] (wq4_gemm_tiled_headmajor)
+  const float* kb = kv + ((size_t)b * H + head) * T * 64 + sub * 4;
+  const size_t vofs = (size_t)gridDim.y * H * T * 64;
+  constexpr int U = 8;  // 32 keys per wave in flight
   for (int j0 = k0; j0 < k1; j0 += 4 * U) {
     floatx4 kk[U], vv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int j = j0 + 4 * u + grp;
-      const bool ok = j < k1;
-      const float* r = kvb + (size_t)(ok ? j : k0) * 2 * D;
-      kk[u] = ok ? *reinterpret_cast<const floatx4*>(r) : floatx4{0.f, 0.f, 0.f, 0.f};
-      vv[u] = ok ? *reinterpret_cast<const floatx4*>(r + D) : floatx4{0.f, 0.f, 0.f, 0.f};
+      const int j = min(j0 + 4 * u + grp, k1 - 1);  // clamped: loads never branch
+      const float* r = kb + (size_t)j * 64;
+      kk[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(r));
+      vv[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(r + vofs));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int j = j0 + 4 * u + grp;
-      const bool ok = j < k1;
+      const bool ok = j0 + 4 * u + grp < k1;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
+      for (int t = 0; t < TQ; ++t) {
         if (t < Tq) {
           float dot = qv[t][0] * kk[u][0] + qv[t][1] * kk[u][1] + qv[t][2] * kk[u][2] + qv[t][3] * kk[u][3];
 #pragma unroll
@@ -383,7 +419,7 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const float* __restrict
   }
   // merge the 4 groups of the wave, then the 4 waves (fixed order)
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < TQ; ++t) {
     if (t >= Tq) break;
 #pragma unroll
     for (int off = 16; off < 64; off <<= 1) {
@@ -408,33 +444,91 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const float* __restrict
     }
   }
   __syncthreads();
+  // wave t merges the 4 waves for query t: (mn, ls, os[lane])
+  float mn = -INFINITY, ls = 0.0f, os = 0.0f;
   if (wave < Tq) {
     const int t = wave;
-    float mn = -INFINITY;
 #pragma unroll
     for (int w = 0; w < 4; ++w) mn = fmaxf(mn, wm[w][t]);
-    float ls = 0.0f, os = 0.0f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       const float a = wm[w][t] == -INFINITY ? 0.0f : expf(wm[w][t] - mn);
       ls += wl[w][t] * a;
       os += wo[w][t][lane] * a;
     }
+  }
+  if (S > 1) {
+    typedef __attribute__((address_space(1))) float gfloat;
+    typedef __attribute__((address_space(1))) int gint;
+    const size_t bh = (size_t)b * H + head;
+    if (wave < Tq) {  // publish this split's partial write-through
+      gfloat* pp = (gfloat*)(part + ((bh * S + split) * 4 + wave) * kXattnPart);
+      __hip_atomic_store(pp + lane, os, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_store(pp + 64, mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 1) __hip_atomic_store(pp + 65, ls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+    __syncthreads();
+    if (tid == 0) {
+      const int prev = __hip_atomic_fetch_add((gint*)(counters + bh), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_flag = prev == S - 1;
+      if (prev == S - 1) __hip_atomic_store((gint*)(counters + bh), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last_flag || wave >= Tq) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: loads stay below the ticket
+    // merge the S partials in split order (sc1 loads of sc1-stored bytes)
+    float pm[kXattnMaxSplit], pl[kXattnMaxSplit], po[kXattnMaxSplit];
+#pragma unroll
+    for (int sp = 0; sp < kXattnMaxSplit; ++sp) {
+      if (sp < S) {
+        gfloat* pp = (gfloat*)(part + ((bh * S + sp) * 4 + wave) * kXattnPart);
+        po[sp] = __hip_atomic_load(pp + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pm[sp] = __hip_atomic_load(pp + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pl[sp] = __hip_atomic_load(pp + 65, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    mn = -INFINITY;
+#pragma unroll
+    for (int sp = 0; sp < kXattnMaxSplit; ++sp)
+      if (sp < S) mn = fmaxf(mn, pm[sp]);
+    ls = 0.0f;
+    os = 0.0f;
+#pragma unroll
+    for (int sp = 0; sp < kXattnMaxSplit; ++sp) {
+      if (sp < S) {
+        const float a = pm[sp] == -INFINITY ? 0.0f : expf(pm[sp] - mn);
+        ls += pl[sp] * a;
+        os += po[sp] * a;
+      }
+    }
+  }
+  if (wave < Tq) {
+    const int t = wave;
     const float val = os / ls;
     const float v1 = __shfl_down(val, 1, 64), v2 = __shfl_down(val, 2, 64), v3 = __shfl_down(val, 3, 64);
     if ((lane & 3) == 0) atile_store4<NS>(tiled, b * Tq + t, head * 64 + lane, kbp_of(D), val, v1, v2, v3);
   }
 }
 
-hipError_t launch_cross_attention(const float* q, const float* kv, int B, int Tq, int T, int H, _Float16* tiled,
-                                  int ns, hipStream_t st) {
+hipError_t launch_cross_attention(const float* q, const float* kv, int B, int Tq, int T, int H, float* part,
+                                  int* counters, _Float16* tiled, int ns, hipStream_t st) {
   if (Tq > 4) return hipErrorInvalidValue;
-  const dim3 grid(H, B), block(256);
-  if (ns == 2)
-    hipLaunchKernelGGL((cross_attn_kernel<2>), grid, block, 0, st, q, kv, Tq, T, H, tiled);
-  else
-    hipLaunchKernelGGL((cross_attn_kernel<1>), grid, block, 0, st, q, kv, Tq, T, H, tiled);
+  const int S = cross_attention_splits(T);
+  const dim3 grid(H * S, B), block(256);
+#define WA_XATTN(NS_, TQ_) \
+  hipLaunchKernelGGL((cross_attn_kernel<NS_, TQ_>), grid, block, 0, st, q, kv, Tq, T, H, S, part, counters, tiled)
+  if (ns == 2) {
+    if (Tq == 1) WA_XATTN(2, 1); else WA_XATTN(2, 4);
+  } else {
+    if (Tq == 1) WA_XATTN(1, 1); else WA_XATTN(1, 4);
+  }
+#undef WA_XATTN
   return hipGetLastError();
+}
+
+size_t cross_attention_part_floats(int B, int H, int T) {
+  return (size_t)B * H * cross_attention_splits(T) * 4 * kXattnPart;
 }
 
 // ------------------------------------------------------ conv + GELU --

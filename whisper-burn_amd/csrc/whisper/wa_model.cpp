@@ -165,12 +165,15 @@ struct wa_model {
   float *h1, *x, *qkv, *xd, *qkvd, *qd, *hid, *logits;
   _Float16 *at_d, *at_f, *enc_at, *atd_dec, *atf_dec;
   int *prompt_tok, *next_tok, *tokens, *ntok, *done;
+  float* xattn_part;     // cross-attention split partials
+  int* xattn_counters;   // per (clip, head) arrival tickets, re-armed in-kernel
   wa::DecodeState* state;
   int* host_ndone = nullptr;  // pinned ring
   // step graph
   hipGraphExec_t graph = nullptr;
   int graph_b = -1;
   hipStream_t graph_stream = nullptr;
+  hipStream_t own_stream = nullptr;  // transcribe runs here (graph capture needs a non-null stream)
   float timings[5] = {0, 0, 0, 0, 0};
   // live kernel timing (wa_profile_*)
   struct Pending {
@@ -200,6 +203,7 @@ struct wa_model {
   ~wa_model() {
     resolve_profile();
     if (graph) (void)hipGraphExecDestroy(graph);
+    if (own_stream) (void)hipStreamDestroy(own_stream);
     if (host_ndone) (void)hipHostFree(host_ndone);
     for (auto& l : enc)
       for (wq4_tensor* t : {l.qkv, l.out, l.fc1, l.fc2}) wq4_tensor_destroy(t);
@@ -376,6 +380,10 @@ wq4_status alloc_activations(wa_model* m) {
   m->ntok = d.alloc<int>(B);
   m->done = d.alloc<int>(B);
   m->state = d.alloc<wa::DecodeState>(1);
+  m->xattn_part = f32((int64_t)wa::cross_attention_part_floats(B, c.n_text_head, T));
+  m->xattn_counters = d.alloc<int>((size_t)B * c.n_text_head);
+  if (!m->xattn_part || !m->xattn_counters) return fail(WQ4_ENOMEM, "cross-attention workspace allocation failed");
+  WA_HIP(hipMemset(m->xattn_counters, 0, (size_t)B * c.n_text_head * sizeof(int)));
   for (void* p : {(void*)m->h1, (void*)m->x, (void*)m->qkv, (void*)m->at_d, (void*)m->at_f, (void*)m->enc_at,
                   (void*)m->xd, (void*)m->qkvd, (void*)m->qd, (void*)m->hid, (void*)m->logits, (void*)m->atd_dec,
                   (void*)m->atf_dec, (void*)m->prompt_tok, (void*)m->next_tok, (void*)m->tokens, (void*)m->ntok,
@@ -480,12 +488,15 @@ wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st,
 }
 
 // Cross-attention K/V of every decoder layer from encoder_out
-// (attention.rs:309-335 forward_init_cache, run once per clip).
+// (attention.rs:177-206 forward_init_cache, run once per clip).
 wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st) {
   const int64_t rows = (int64_t)B * m->cfg.n_audio_ctx;
   for (auto& L : m->dec) {
     Prof p = q4prof(m, st, L.ckv, rows);
-    WA_WQ4(wq4_gemm_tiled(L.ckv, L.ckv_b, m->enc_at, nullptr, L.cross_kv, nullptr, rows, 0u, m->prec, 1, st));
+    // K|V written head-major [2][B][H][T][64]: each (clip, head) streams two
+    // contiguous 384 KB ranges in the decode steps' cross-attention
+    WA_WQ4(wq4_gemm_tiled_headmajor(L.ckv, L.ckv_b, m->enc_at, L.cross_kv, rows, m->cfg.n_audio_ctx,
+                                    m->cfg.n_text_state, m->prec, 1, st));
   }
   return WQ4_OK;
 }
@@ -506,7 +517,8 @@ wq4_status decoder_forward(wa_model* m, const int* tokens, int B, int Tq, const 
     WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, m->atd_dec, m->xd, m->xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
     WA_HIP(wa::launch_layernorm(m->xd, L.ln2_w, L.ln2_b, (int)rows, D, m->atd_dec, m->ns, nullptr, st));
     WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, m->atd_dec, nullptr, m->qd, nullptr, rows, 0u, m->prec, 2, st));
-    WA_HIP(wa::launch_cross_attention(m->qd, L.cross_kv, B, Tq, c.n_audio_ctx, H, m->atd_dec, m->ns, st));
+    WA_HIP(wa::launch_cross_attention(m->qd, L.cross_kv, B, Tq, c.n_audio_ctx, H, m->xattn_part, m->xattn_counters,
+                                      m->atd_dec, m->ns, st));
     WA_WQ4(wq4_gemm_tiled(L.cout, L.cout_b, m->atd_dec, m->xd, m->xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2,
                           st));
     WA_HIP(wa::launch_layernorm(m->xd, L.ln3_w, L.ln3_b, (int)rows, D, m->atd_dec, m->ns, nullptr, st));
@@ -562,6 +574,8 @@ wq4_status wa_model_create_synthetic(int device, int variant, uint64_t seed, int
   if (s != WQ4_OK) return s;
   s = alloc_activations(m.get());
   if (s != WQ4_OK) return s;
+  WA_HIP(hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking));
+  WA_HIP(hipDeviceSynchronize());
   *out = m.release();
   return WQ4_OK;
 }
@@ -628,7 +642,8 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
   if (n_clips < 1 || n_clips > m->bmax) return fail(WQ4_EINVAL, "n_clips out of range");
   if (max_tokens < 1 || max_tokens > kMaxTokens) return fail(WQ4_EINVAL, "max_tokens must be in [1, 224]");
   WA_HIP(hipSetDevice(m->device));
-  hipStream_t st = static_cast<hipStream_t>(stream);
+  // all work on the model's own stream, ordered after the caller's stream
+  hipStream_t st = m->own_stream;
   const Config& c = m->cfg;
   const int B = n_clips;
   hipEvent_t ev[5];
@@ -639,6 +654,8 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
       for (int i = 0; i < 5; ++i) (void)hipEventDestroy(e[i]);
     }
   } evg{ev};
+  WA_HIP(hipEventRecord(ev[4], static_cast<hipStream_t>(stream)));
+  WA_HIP(hipStreamWaitEvent(st, ev[4], 0));
 
   WA_HIP(hipEventRecord(ev[0], st));
   wq4_status s = encoder_forward(m, mel_dev, B, st, nullptr);

@@ -93,13 +93,44 @@ wq4_status arena_get(int dev, void* stream, size_t need, void** out) {
   return WQ4_OK;
 }
 
+// Split-K workspace of the decode kernel per (device, stream); never freed
+// (tiny, and kernels in flight or captured graphs may still reference it).
+std::map<std::pair<int, void*>, wq4::DecodeWs> g_decode_ws;
+
+wq4_status decode_ws_get(int dev, void* stream, const wq4::DecodeWs** out) {
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  auto it = g_decode_ws.find({dev, stream});
+  if (it == g_decode_ws.end()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(static_cast<hipStream_t>(stream), &cs) == hipSuccess &&
+        cs != hipStreamCaptureStatusNone)
+      return fail(WQ4_EINVAL,
+                  "the first small-M GEMM on a stream must run outside graph capture (it allocates the split-K "
+                  "workspace)");
+    wq4::DecodeWs ws{nullptr, nullptr};
+    hipError_t e = hipMalloc(&ws.part, (size_t)wq4::kDecodeWsFloats * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&ws.counters, (size_t)wq4::kDecodeMaxTiles * sizeof(int));
+    if (e == hipSuccess)
+      e = hipMemsetAsync(ws.counters, 0, (size_t)wq4::kDecodeMaxTiles * sizeof(int),
+                         static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) {
+      if (ws.part) (void)hipFree(ws.part);
+      if (ws.counters) (void)hipFree(ws.counters);
+      return fail(WQ4_ENOMEM, std::string("decode workspace: ") + hipGetErrorString(e));
+    }
+    it = g_decode_ws.emplace(std::make_pair(dev, stream), ws).first;
+  }
+  *out = &it->second;
+  return WQ4_OK;
+}
+
 int ns_of(wq4_precision p) { return p == WQ4_PREC_F16 ? 1 : 2; }
 
 bool use_decode(int64_t rows) {
   const int pol = g_policy.load();
   if (pol == 1) return false;
   if (pol == 2) return true;
-  return rows <= 64;
+  return rows <= 32 * wq4::kDecodeMaxMTiles;
 }
 
 wq4::EpiArgs make_epi(const float* bias, const float* residual, float* out, int ldo, int m, int n, bool gelu) {
@@ -129,9 +160,16 @@ wq4_status check_gemm_tensor(const wq4_tensor* w) {
   return WQ4_OK;
 }
 
-hipError_t gemm(const wq4_tensor* w, const _Float16* at, int64_t rows, const wq4::EpiArgs& e, int mode, int ns,
-                hipStream_t st) {
-  return wq4::launch_q4_gemm(w->g, w->nib, w->sc, w->cs, at, (int)rows, e, mode, ns, use_decode(rows), st);
+wq4_status gemm(const wq4_tensor* w, const _Float16* at, int64_t rows, const wq4::EpiArgs& e, int mode, int ns,
+                hipStream_t st, bool dec) {
+  const wq4::DecodeWs* ws = nullptr;
+  if (dec) {
+    wq4_status s = decode_ws_get(w->device, st, &ws);
+    if (s != WQ4_OK) return s;
+  }
+  hipError_t he = wq4::launch_q4_gemm(w->g, w->nib, w->sc, w->cs, at, (int)rows, e, mode, ns, ws, st);
+  if (he != hipSuccess) return hip_fail(he, "q4_gemm launch");
+  return WQ4_OK;
 }
 
 }  // namespace
@@ -317,9 +355,7 @@ static wq4_status linear_impl(const wq4_tensor* w, const float* bias, const floa
   if (e != hipSuccess) return hip_fail(e, "tile_activations launch");
   wq4::EpiArgs epi = make_epi(bias, (flags & WQ4_EPI_RESIDUAL) ? residual : nullptr, y, (int)w->g.n, (int)rows,
                               (int)w->g.n, (flags & WQ4_EPI_GELU) != 0);
-  e = gemm(w, at, rows, epi, wq4::kEpiF32, ns, st);
-  if (e != hipSuccess) return hip_fail(e, "q4_gemm launch");
-  return WQ4_OK;
+  return gemm(w, at, rows, epi, wq4::kEpiF32, ns, st, use_decode(rows));
 }
 
 wq4_status wq4_linear_forward_ws(const wq4_tensor* w, const float* bias_dev, const float* x_dev,
@@ -383,13 +419,11 @@ static wq4_status ffn_impl(const wq4_tensor* fc1, const float* b1, const wq4_ten
   wq4::EpiArgs e1 = make_epi(b1, nullptr, nullptr, (int)fc1->g.n, (int)rows, (int)fc1->g.n, true);
   e1.out_tiled = a2;
   e1.nbp_next = (int)fc2->g.nbp;
-  e = gemm(fc1, a1, rows, e1, wq4::kEpiTiled, ns, st);
-  if (e != hipSuccess) return hip_fail(e, "fc1 launch");
+  wq4_status s1 = gemm(fc1, a1, rows, e1, wq4::kEpiTiled, ns, st, use_decode(rows));
+  if (s1 != WQ4_OK) return s1;
   wq4::EpiArgs e2 = make_epi(b2, (flags & WQ4_EPI_RESIDUAL) ? residual : nullptr, y, (int)fc2->g.n, (int)rows,
                              (int)fc2->g.n, (flags & WQ4_EPI_GELU) != 0);
-  e = gemm(fc2, a2, rows, e2, wq4::kEpiF32, ns, st);
-  if (e != hipSuccess) return hip_fail(e, "fc2 launch");
-  return WQ4_OK;
+  return gemm(fc2, a2, rows, e2, wq4::kEpiF32, ns, st, use_decode(rows));
 }
 
 wq4_status wq4_ffn_forward_ws(const wq4_tensor* fc1, const float* b1_dev, const wq4_tensor* fc2,
@@ -453,10 +487,8 @@ wq4_status wq4_linear_forward_tiled(const wq4_tensor* w, const float* bias_dev, 
   DeviceGuard dg(w->device);
   wq4::EpiArgs epi = make_epi(bias_dev, (flags & WQ4_EPI_RESIDUAL) ? residual_dev : nullptr, y_dev, (int)w->g.n,
                               (int)rows, (int)w->g.n, (flags & WQ4_EPI_GELU) != 0);
-  hipError_t e = gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, wq4::kEpiF32, ns_of(prec),
-                      static_cast<hipStream_t>(stream));
-  if (e != hipSuccess) return hip_fail(e, "q4_gemm launch");
-  return WQ4_OK;
+  return gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, wq4::kEpiF32, ns_of(prec),
+              static_cast<hipStream_t>(stream), use_decode(rows));
 }
 
 wq4_status wq4_linear_forward_tiled_out(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
@@ -478,10 +510,8 @@ wq4_status wq4_linear_forward_tiled_out(const wq4_tensor* w, const float* bias_d
                               (flags & WQ4_EPI_GELU) != 0);
   epi.out_tiled = static_cast<_Float16*>(at_out_dev);
   epi.nbp_next = (int)((w->g.n / 32 + 1) / 2);
-  hipError_t e = gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, wq4::kEpiTiled, ns_of(prec),
-                      static_cast<hipStream_t>(stream));
-  if (e != hipSuccess) return hip_fail(e, "q4_gemm launch");
-  return WQ4_OK;
+  return gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, wq4::kEpiTiled, ns_of(prec),
+              static_cast<hipStream_t>(stream), use_decode(rows));
 }
 
 wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void* at_dev, const float* residual_dev,
@@ -507,11 +537,31 @@ wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void
     epi.nbp_next = (int)((w->g.n / 32 + 1) / 2);
   }
   const bool dec = kernel == 0 ? use_decode(rows) : kernel == 2;
-  hipError_t e = wq4::launch_q4_gemm(w->g, w->nib, w->sc, w->cs, static_cast<const _Float16*>(at_dev), (int)rows,
-                                     epi, tiled_out ? wq4::kEpiTiled : wq4::kEpiF32, ns_of(prec), dec,
-                                     static_cast<hipStream_t>(stream));
-  if (e != hipSuccess) return hip_fail(e, "q4_gemm launch");
-  return WQ4_OK;
+  return gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, tiled_out ? wq4::kEpiTiled : wq4::kEpiF32,
+              ns_of(prec), static_cast<hipStream_t>(stream), dec);
+}
+
+wq4_status wq4_gemm_tiled_headmajor(const wq4_tensor* w, const float* bias_dev, const void* at_dev, float* y_dev,
+                                    int64_t rows, int group_rows, int d, wq4_precision prec, int kernel,
+                                    void* stream) {
+  wq4_status s = check_gemm_tensor(w);
+  if (s != WQ4_OK) return s;
+  s = check_prec(prec);
+  if (s != WQ4_OK) return s;
+  if (kernel < 0 || kernel > 2) return fail(WQ4_EINVAL, "kernel must be 0, 1 or 2");
+  if (rows < 0 || rows > (1 << 24)) return fail(WQ4_ESHAPE, "bad row count");
+  if (group_rows <= 0 || rows % group_rows != 0) return fail(WQ4_ESHAPE, "rows must be a multiple of group_rows");
+  if (d <= 0 || d % 64 != 0 || w->g.n % d != 0)
+    return fail(WQ4_ESHAPE, "head-major output needs d % 64 == 0 and N % d == 0");
+  if (rows == 0) return WQ4_OK;
+  if (!at_dev || !y_dev) return fail(WQ4_EINVAL, "null argument");
+  DeviceGuard dg(w->device);
+  wq4::EpiArgs epi = make_epi(bias_dev, nullptr, y_dev, (int)w->g.n, (int)rows, (int)w->g.n, false);
+  epi.hm_t = group_rows;
+  epi.hm_d = d;
+  const bool dec = kernel == 0 ? use_decode(rows) : kernel == 2;
+  return gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, wq4::kEpiHeadMajor, ns_of(prec),
+              static_cast<hipStream_t>(stream), dec);
 }
 
 // scripts/convert_whisper.py:33-74 (numpy 2 scalar semantics: amax, d in f32).

@@ -1,5 +1,6 @@
 // wq4_epi.hpp -- epilogue description shared by host launchers and kernels.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace wq4 {
@@ -14,8 +15,24 @@ struct EpiArgs {
   int gelu;               // tanh-GELU after bias (layers.rs:35-41)
   int m;                  // real rows
   int n;                  // real cols
+  int hm_t;               // > 0: head-major f32 output, rows grouped by hm_t (see out_index)
+  int hm_d;               //      columns per part (K | V), heads of 64
 };
 
-enum EpiMode { kEpiF32 = 0, kEpiTiled = 1 };
+// Output element index.  Row-major by default; head-major (hm_t > 0) writes
+// out[part][g][head][t][64] for row = g * hm_t + t, col = part * hm_d +
+// head * 64 + d -- the [B, H, T, 64] K/V view the attention reads
+// (reference: src/model/attention.rs:254-263, reshape + swap_dims of k, v).
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline size_t out_index(const EpiArgs& e, int row, int col) {
+  if (e.hm_t <= 0) return (size_t)row * e.ldo + col;
+  const int g = row / e.hm_t, t = row - g * e.hm_t;
+  const int part = col / e.hm_d, c = col - part * e.hm_d;
+  return (size_t)part * e.m * e.hm_d + (((size_t)g * (e.hm_d >> 6) + (c >> 6)) * e.hm_t + t) * 64 + (c & 63);
+}
+
+enum EpiMode { kEpiF32 = 0, kEpiTiled = 1, kEpiHeadMajor = 2 };  // head-major: f32 via out_index
 
 }  // namespace wq4

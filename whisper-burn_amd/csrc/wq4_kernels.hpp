@@ -11,10 +11,28 @@ namespace wq4 {
 // f32 [M, ld] row-major -> A-tiled f16 split (ns = 1 or 2).
 hipError_t launch_tile_activations(const float* x, _Float16* at, int M, int K, int ld, int ns, hipStream_t st);
 
+// Split-K workspace of the decode kernel, one per (device, stream): partial
+// tiles and per-n-tile arrival counters (zeroed once, re-armed by the kernel).
+constexpr int64_t kDecodeWsFloats = (int64_t)4 << 20;  // 16 MiB of partials
+constexpr int64_t kDecodeMaxTiles = 1 << 16;            // counters
+constexpr int kDecodeMaxPer = 4;                        // block pairs per wave
+constexpr int kDecodeMaxMTiles = 4;                     // rows <= 128 (launches of 2 m-tiles)
+struct DecodeWs {
+  float* part;
+  int* counters;
+};
+struct DecodePlan {
+  int per;    // kernel instance: max block pairs per wave
+  int ks;     // workgroups (K slices) per n-tile
+  int chunk;  // block pairs per wave (<= per)
+};
+DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal);
+
 // y = epi((A W^T) * colscale).  epi_mode: 0 = f32 row-major, 1 = A-tiled f16
-// operand of a following GEMM.  decode selects the K-split kernel.
+// operand of a following GEMM.  ws != null selects the split-K decode kernel
+// (rows <= 128; larger row counts or unsupported shapes use the tile kernel).
 hipError_t launch_q4_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* colscale,
-                          const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int ns, bool decode,
+                          const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int ns, const DecodeWs* ws,
                           hipStream_t st);
 
 }  // namespace wq4

@@ -25,6 +25,8 @@
 // on M or the tile position: a row's result is identical at batch 1 and 256.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "wq4_device.hpp"
 #include "wq4_kernels.hpp"
 
@@ -257,6 +259,38 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
               e.out[(size_t)row * e.ldo + col] = epi_value(acc[mt][nt][i] * cs[nt], row, col, e);
           }
     }
+  } else if constexpr (EPI == kEpiHeadMajor) {
+    if (active) {
+      // one division per m-tile and n-tile, not per element (out_index)
+      size_t cofs[TN];
+#pragma unroll
+      for (int nt = 0; nt < TN; ++nt) {
+        const int col = (nt0 + nt) * 32 + r;
+        const int part = col / e.hm_d, c = col - part * e.hm_d;
+        cofs[nt] = (size_t)part * e.m * e.hm_d + (size_t)(c >> 6) * e.hm_t * 64 + (c & 63);
+      }
+      const size_t gstride = (size_t)(e.hm_d >> 6) * e.hm_t * 64;
+#pragma unroll
+      for (int mt = 0; mt < TM; ++mt) {
+        const int r0 = (TM * mg + mt) * 32;
+        const int g0 = r0 / e.hm_t, t0 = r0 - g0 * e.hm_t;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int rl = acc_row(i, h), row = r0 + rl;
+          int t = t0 + rl, g = g0;
+          while (t >= e.hm_t) {  // at most one step when hm_t >= 32
+            t -= e.hm_t;
+            ++g;
+          }
+          const size_t rofs = (size_t)g * gstride + (size_t)t * 64;
+#pragma unroll
+          for (int nt = 0; nt < TN; ++nt) {
+            const int col = (nt0 + nt) * 32 + r;
+            if (row < e.m && col < e.n) e.out[rofs + cofs[nt]] = epi_value(acc[mt][nt][i] * cs[nt], row, col, e);
+          }
+        }
+      }
+    }
   } else {
     float* stage = reinterpret_cast<float*>(smem) + wave * (32 * kStageLd);
 #pragma unroll
@@ -281,133 +315,222 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
 }
 
 // ------------------------------------------------------------------------
-// Decode / small-M kernel.
+// Decode / small-M kernel (M <= 64: decoder tokens, prompt).
+//
+// Latency-bound GEMV-like shape: the weight bytes of one launch (~1-4 MB)
+// are far too few to fill HBM from a handful of workgroups, and every output
+// column needs the whole activation operand.  So the K range is split twice:
+//   * over KS workgroups per 32-column n-tile (grid = ntiles * KS, chosen so
+//     the grid covers most of the 256 CUs), and
+//   * over the 4 waves of a workgroup (<= PER block pairs per wave).
+// Every wave issues all of its weight and activation loads at once (one
+// memory latency, no serial prefetch chain), runs two MFMA chains (k-half
+// kk = 0 / 1), and the wave partials are summed through LDS in wave order.
+// With KS > 1 each workgroup stores its 32 x 32 partial to a workspace; the
+// last workgroup of the n-tile to arrive (device-scope counter) sums the KS
+// partials in slice order, applies the epilogue and re-arms the counter.
+// Summation order is a function of (N, K) only -> deterministic and batch
+// invariant.
 // ------------------------------------------------------------------------
-constexpr int kDecodeMTG = 2;     // m-tiles held in registers per pass
-constexpr int kDecodeWaves = 8;   // waves per workgroup, each a contiguous K range
-constexpr int kDecodeMaxBp = 12;  // block pairs whose weights a wave keeps in flight
+constexpr int kDecodeWaves = 4;
+constexpr int kDecodeMaxKs = 8;  // K slices per n-tile (fix-up keeps all slabs in flight)
+
+// Branch-free loads through buffer resources: an out-of-range offset reads
+// zeros, so masked rows and the ragged end of a wave's K range need no exec
+// branches (which would make the compiler drain vmcnt between load groups).
+constexpr int kOob = 0x7fffff00;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+template <int AUX>
+__device__ __forceinline__ half8 bload_h8(__amdgpu_buffer_rsrc_t rs, int off) {
+  return __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUX));
+}
 
 template <int NS, int EPI>
-__global__ __launch_bounds__(512) void q4_gemm_decode_kernel(const uint8_t* __restrict__ nib,
-                                                             const uint32_t* __restrict__ sc,
-                                                             const float* __restrict__ colscale,
-                                                             const _Float16* __restrict__ at, int mtiles,
-                                                             int nbp, int ntiles, EpiArgs e) {
+__device__ __forceinline__ void decode_epilogue(const floatx16& s, float cs, int mt, int nt, int lane, float* stage,
+                                                const EpiArgs& e) {
+  const int r = lane & 31, h = lane >> 5;
+  const int col = nt * 32 + r;
+  if constexpr (EPI != kEpiTiled) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = mt * 32 + acc_row(i, h);
+      if (row < e.m && col < e.n)
+        e.out[EPI == kEpiHeadMajor ? out_index(e, row, col) : (size_t)row * e.ldo + col] =
+            epi_value(s[i] * cs, row, col, e);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int rl = acc_row(i, h);
+      const int row = mt * 32 + rl;
+      stage[rl * kStageLd + r] = (row < e.m && col < e.n) ? epi_value(s[i] * cs, row, col, e) : 0.0f;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): stage writes visible to this wave
+    __builtin_amdgcn_wave_barrier();
+    store_tiled_slab<NS, 1>(stage, e, mt, nt, lane);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int NS, int EPI, int PER, int MT>
+__global__ __launch_bounds__(256) void q4_gemm_decode_kernel(const uint8_t* __restrict__ nib,
+                                                              const uint32_t* __restrict__ sc,
+                                                              const float* __restrict__ colscale,
+                                                              const _Float16* __restrict__ at, int mt0, int nbp, int ks,
+                                                              int chunk, float* __restrict__ part,
+                                                              int* __restrict__ counters, EpiArgs e) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int W = kDecodeWaves;
+  constexpr int mtiles = MT;
   float* red = reinterpret_cast<float*>(smem);                        // [W-1][16][64]
   float* stage = reinterpret_cast<float*>(smem) + (W - 1) * 16 * 64;  // [32][kStageLd]
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int nt = blockIdx.x;
-  const int chunk = (nbp + W - 1) / W;
-  const int bp0 = wave * chunk;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar buffer descriptors
+  const int r = lane & 31;
+  const int nt = blockIdx.x / ks;
+  const int slice = blockIdx.x - nt * ks;
+  const int bp0 = min(nbp, (slice * W + wave) * chunk);  // chunk <= PER (launcher)
   const int cnt = max(0, min(nbp, bp0 + chunk) - bp0);
-  const size_t kbp = (size_t)nbp * 2;
-  const half8* afr = reinterpret_cast<const half8*>(at);
   const float cs = colscale[nt * 32 + r];
 
-  for (int mt0 = 0; mt0 < mtiles; mt0 += kDecodeMTG) {
-    floatx16 acc[kDecodeMTG];
+  // this wave's weights (once-read stream: nt) -- zeros past cnt
+  const size_t t0 = (size_t)nt * nbp + bp0;
+  const __amdgpu_buffer_rsrc_t rw = brsrc(nib + t0 * 1024, (uint32_t)cnt * 1024);
+  const __amdgpu_buffer_rsrc_t rsc = brsrc(sc + t0 * 32, (uint32_t)cnt * 128);
+  u32x4 br[PER];
+  uint32_t bs[PER];
 #pragma unroll
-    for (int a = 0; a < kDecodeMTG; ++a)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[a][i] = 0.0f;
-
-    for (int base = 0; base < cnt; base += kDecodeMaxBp) {
-      const int n = min(kDecodeMaxBp, cnt - base);
-      // every weight load of this pass in flight at once (memory-level parallelism)
-      u32x4 br[kDecodeMaxBp];
-      uint32_t bs[kDecodeMaxBp];
-#pragma unroll
-      for (int i = 0; i < kDecodeMaxBp; ++i) {
-        if (i < n) {
-          const size_t t = (size_t)nt * nbp + bp0 + base + i;
-          br[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(nib + (t * 64 + lane) * 16));
-          bs[i] = __builtin_nontemporal_load(sc + t * 32 + r);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < kDecodeMaxBp; ++i) {
-        if (i < n) {
-          const int bp = bp0 + base + i;
-#pragma unroll
-          for (int blk = 0; blk < 2; ++blk) {
-            const uint32_t dbits = blk ? (bs[i] >> 16) : (bs[i] & 0xffffu);
-            half8 bh[2], bl[2];
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) deq_scaled<NS>(br[i][blk * 2 + kk], dbits, bh[kk], bl[kk]);
-#pragma unroll
-            for (int mi = 0; mi < kDecodeMTG; ++mi) {
-              const int mt = mt0 + mi;
-              if (mt < mtiles) {
-                const bool row_ok = mt * 32 + r < e.m;
-#pragma unroll
-                for (int kk = 0; kk < 2; ++kk) {
-                  const size_t frag = (((size_t)mt * kbp + 2 * bp + blk) * 2 + kk) * NS;
-                  half8 ahi, alo;
-#pragma unroll
-                  for (int j = 0; j < 8; ++j) {
-                    ahi[j] = (_Float16)0.0f;
-                    alo[j] = (_Float16)0.0f;
-                  }
-                  if (row_ok) {
-                    ahi = afr[frag * 64 + lane];
-                    if constexpr (NS == 2) alo = afr[(frag + 1) * 64 + lane];
-                  }
-                  acc[mi] = mfma32(ahi, bh[kk], acc[mi]);
-                  if constexpr (NS == 2) {
-                    acc[mi] = mfma32(alo, bh[kk], acc[mi]);
-                    acc[mi] = mfma32(ahi, bl[kk], acc[mi]);
-                  }
-                }
-              }
-            }
-          }
-        }
-      }
-    }
-
-    // Fixed-order reduction over the W waves, one m-tile at a time.
-#pragma unroll
-    for (int mi = 0; mi < kDecodeMTG; ++mi) {
-      const int mt = mt0 + mi;
-      if (mt >= mtiles) break;  // uniform across the workgroup
-      if (wave > 0) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) red[((wave - 1) * 16 + i) * 64 + lane] = acc[mi][i];
-      }
-      __syncthreads();
-      if (wave == 0) {
-        floatx16 s = acc[mi];
-#pragma unroll
-        for (int w = 0; w < W - 1; ++w)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) s[i] = s[i] + red[(w * 16 + i) * 64 + lane];
-        if constexpr (EPI == kEpiF32) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int row = mt * 32 + acc_row(i, h);
-            const int col = nt * 32 + r;
-            if (row < e.m && col < e.n) e.out[(size_t)row * e.ldo + col] = epi_value(s[i] * cs, row, col, e);
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int rl = acc_row(i, h);
-            const int row = mt * 32 + rl;
-            const int col = nt * 32 + r;
-            stage[rl * kStageLd + r] = (row < e.m && col < e.n) ? epi_value(s[i] * cs, row, col, e) : 0.0f;
-          }
-          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): stage writes visible to this wave
-          __builtin_amdgcn_wave_barrier();
-          store_tiled_slab<NS, 1>(stage, e, mt, nt, lane);
-        }
-      }
-      __syncthreads();
-    }
+  for (int i = 0; i < PER; ++i) {
+    br[i] = __builtin_amdgcn_raw_buffer_load_b128(rw, (i * 64 + lane) * 16, 0, 2);
+    bs[i] = __builtin_amdgcn_raw_buffer_load_b32(rsc, (i * 32 + r) * 4, 0, 2);
   }
+  // activation fragments of every m-tile, rows >= M read as zeros
+  const size_t slab = (size_t)nbp * 2 * 2 * NS * 1024;  // bytes of one m-tile (kbp = 2 nbp)
+  half8 a[MT][PER][2][2][NS];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const __amdgpu_buffer_rsrc_t ra = brsrc(reinterpret_cast<const uint8_t*>(at) + (mt0 + mt) * slab + (size_t)bp0 * 4 * NS * 1024,
+                                            (uint32_t)cnt * 4 * NS * 1024);
+    const bool row_ok = (mt0 + mt) * 32 + r < e.m;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int q = 0; q < NS; ++q) {
+            const int frag = ((2 * i + blk) * 2 + kk) * NS + q;
+            a[mt][i][blk][kk][q] = bload_h8<0>(ra, row_ok ? frag * 1024 + lane * 16 : kOob);
+          }
+  }
+
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    floatx16 acc0, acc1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      acc0[i] = 0.0f;
+      acc1[i] = 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if (i < cnt) {
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk) {
+          const uint32_t dbits = blk ? (bs[i] >> 16) : (bs[i] & 0xffffu);
+          half8 bh0, bl0, bh1, bl1;
+          deq_scaled<NS>(br[i][blk * 2 + 0], dbits, bh0, bl0);
+          deq_scaled<NS>(br[i][blk * 2 + 1], dbits, bh1, bl1);
+          acc0 = mfma32(a[mt][i][blk][0][0], bh0, acc0);
+          acc1 = mfma32(a[mt][i][blk][1][0], bh1, acc1);
+          if constexpr (NS == 2) {
+            acc0 = mfma32(a[mt][i][blk][0][1], bh0, acc0);
+            acc1 = mfma32(a[mt][i][blk][1][1], bh1, acc1);
+            acc0 = mfma32(a[mt][i][blk][0][0], bl0, acc0);
+            acc1 = mfma32(a[mt][i][blk][1][0], bl1, acc1);
+          }
+        }
+      }
+    }
+    floatx16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = acc0[i] + acc1[i];
+
+    // fixed-order reduction over the W waves
+    if (wave > 0) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[((wave - 1) * 16 + i) * 64 + lane] = acc[i];
+    }
+    __syncthreads();
+    if (wave == 0) {
+      floatx16 s = acc;
+#pragma unroll
+      for (int w = 0; w < W - 1; ++w)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[i] = s[i] + red[(w * 16 + i) * 64 + lane];
+      if (ks == 1) {
+        decode_epilogue<NS, EPI>(s, cs, mt0 + mt, nt, lane, stage, e);
+      } else {
+        // write-through (sc1) slab stores: visible device-wide once drained,
+        // no release fence (cdna_hip_programming.md Guideline 16, R1)
+        const __amdgpu_buffer_rsrc_t rs = brsrc(part + (((size_t)nt * mtiles + mt) * ks + slice) * 1024, 4096);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          // whole-vector bit casts only: clang's __builtin_bit_cast of an
+          // ext-vector ELEMENT reads element 0 (ROCm 7.2)
+          const floatx4 f = {s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f), rs, (q * 64 + lane) * 16, 0, 16);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (ks == 1 || wave != 0) return;
+
+  // split-K fix-up: wave 0 of each slice drained its sc1 stores, one ticket
+  // per slice; the slice drawing ks-1 sums all slabs in slice order with sc1
+  // loads (no acquire needed: every handed-off byte is stored and loaded sc1).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  typedef __attribute__((address_space(1))) int gint;
+  gint* ctr = (gint*)(counters + nt);
+  int prev = 0;
+  if (lane == 0) prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  prev = __shfl(prev, 0);
+  if (prev != ks - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep the loads below the ticket
+#pragma unroll
+  for (int mt = 0; mt < mtiles; ++mt) {
+    const __amdgpu_buffer_rsrc_t rs = brsrc(part + ((size_t)nt * mtiles + mt) * ks * 1024, (uint32_t)ks * 4096);
+    u32x4 v[kDecodeMaxKs][4];  // every slab load in flight at once
+#pragma unroll
+    for (int sl = 0; sl < kDecodeMaxKs; ++sl)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        v[sl][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, sl < ks ? sl * 4096 + (q * 64 + lane) * 16 : kOob, 0, 16);
+    floatx16 s;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const floatx4 f = __builtin_bit_cast(floatx4, v[0][q]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s[4 * q + j] = f[j];
+    }
+#pragma unroll
+    for (int sl = 1; sl < kDecodeMaxKs; ++sl)
+      if (sl < ks) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const floatx4 f = __builtin_bit_cast(floatx4, v[sl][q]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s[4 * q + j] = s[4 * q + j] + f[j];
+        }
+      }
+    decode_epilogue<NS, EPI>(s, cs, mt0 + mt, nt, lane, stage, e);
+  }
+  if (lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
 }
 
 // ------------------------------------------------------------------------
@@ -421,6 +544,45 @@ static size_t prefill_lds_bytes(int ns, int epi) {
 
 static size_t decode_lds_bytes() {
   return (size_t)(kDecodeWaves - 1) * 16 * 64 * 4 + (size_t)32 * kStageLd * 4;
+}
+
+DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal) {
+  // Smallest per-wave depth whose grid still covers ~all CUs, then balance.
+  static const int pers[3] = {4, 2, 1};
+  DecodePlan p{1, 1, 1};
+  (void)mreal;  // the plan depends on (N, K) only: batch-invariant rows
+  const int max_per = kDecodeMaxPer;
+  int per = 1;
+  for (int c : pers) {
+    if (c > max_per) continue;
+    const int64_t ks = (nbp + (int64_t)kDecodeWaves * c - 1) / ((int64_t)kDecodeWaves * c);
+    if (ntiles * ks >= 192) {
+      per = c;
+      break;
+    }
+  }
+  static const int forced = [] {  // tuning knob (tools/q4_bench.py)
+    const char* env = getenv("WQ4_DECODE_PER");
+    const int v = env ? atoi(env) : 0;
+    return (v == 1 || v == 2 || v == 4) ? v : 0;
+  }();
+  if (forced) per = forced > max_per ? max_per : forced;
+  static const int64_t max_ks = [] {  // tuning knob: cap the K slices (1 = no split)
+    const char* env = getenv("WQ4_DECODE_MAXKS");
+    const int v = env ? atoi(env) : 0;
+    return (int64_t)(v > 0 ? v : 1 << 20);
+  }();
+  int64_t ks = (nbp + (int64_t)kDecodeWaves * per - 1) / ((int64_t)kDecodeWaves * per);
+  if (ks > max_ks) ks = max_ks;
+  if (ks > kDecodeMaxKs) ks = kDecodeMaxKs;
+  while (ks > 1 && ntiles * ks * 2 * 1024 > (int64_t)kDecodeWsFloats) --ks;  // workspace bound (2 m-tiles)
+  if (ntiles > kDecodeMaxTiles) ks = 1;
+  int64_t chunk = (nbp + (int64_t)kDecodeWaves * ks - 1) / ((int64_t)kDecodeWaves * ks);
+  while (chunk > per) per *= 2;  // ks shrank: deepen the waves
+  p.per = per;
+  p.ks = (int)ks;
+  p.chunk = (int)chunk;
+  return p;
 }
 
 hipError_t launch_tile_activations(const float* x, _Float16* at, int M, int K, int ld, int ns, hipStream_t st) {
@@ -443,12 +605,31 @@ hipError_t launch_tile_activations(const float* x, _Float16* at, int M, int K, i
 
 template <int NS, int EPI>
 static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* cs,
-                                const _Float16* at, int rows, const EpiArgs& e, bool decode, hipStream_t st) {
+                                const _Float16* at, int rows, const EpiArgs& e, const DecodeWs* ws,
+                                hipStream_t st) {
   const int mtiles = (int)(round_up(rows < 1 ? 1 : rows, kMPad) / kMTile);
-  if (decode) {
-    const int mreal = (int)((rows + kMTile - 1) / kMTile);  // never touch padded m-tiles
-    hipLaunchKernelGGL((q4_gemm_decode_kernel<NS, EPI>), dim3((unsigned)g.ntiles), dim3(64 * kDecodeWaves),
-                       decode_lds_bytes(), st, nib, sc, cs, at, mreal, (int)g.nbp, (int)g.ntiles, e);
+  const int mreal0 = (int)((rows + kMTile - 1) / kMTile);
+  if (ws && mreal0 <= kDecodeMaxMTiles && plan_decode(g.ntiles, g.nbp, 2).per <= kDecodeMaxPer) {
+    const DecodePlan p = plan_decode(g.ntiles, g.nbp, 2);
+    const dim3 grid((unsigned)(g.ntiles * p.ks));
+#define WQ4_DEC(PER_, MT_)                                                                                   \
+  hipLaunchKernelGGL((q4_gemm_decode_kernel<NS, EPI, PER_, MT_>), grid, dim3(64 * kDecodeWaves),              \
+                     decode_lds_bytes(), st, nib, sc, cs, at, mt0, (int)g.nbp, p.ks, p.chunk, ws->part,           \
+                     ws->counters, e)
+    // m-tiles in launches of <= 2 (each launch completes before the next on
+    // this stream, so they share the workspace and counters)
+    for (int mt0 = 0; mt0 < mreal0; mt0 += 2) {
+      if (mreal0 - mt0 == 1) {
+        if (p.per == 1) WQ4_DEC(1, 1);
+        else if (p.per == 2) WQ4_DEC(2, 1);
+        else WQ4_DEC(4, 1);
+      } else {
+        if (p.per == 1) WQ4_DEC(1, 2);
+        else if (p.per == 2) WQ4_DEC(2, 2);
+        else WQ4_DEC(4, 2);
+      }
+    }
+#undef WQ4_DEC
   } else {
     const int ngroups = (int)((g.ntiles + 4 * kPrefillTN - 1) / (4 * kPrefillTN));
     const int mgroups = mtiles / kPrefillTM;
@@ -459,14 +640,17 @@ static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint3
 }
 
 hipError_t launch_q4_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* colscale,
-                          const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int ns, bool decode,
+                          const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int ns, const DecodeWs* ws,
                           hipStream_t st) {
-  if (ns == 2) {
-    return epi_mode == kEpiF32 ? launch_gemm_t<2, kEpiF32>(g, nib, sc, colscale, at, rows, e, decode, st)
-                               : launch_gemm_t<2, kEpiTiled>(g, nib, sc, colscale, at, rows, e, decode, st);
+#define WQ4_GEMM(NS_)                                                                                        \
+  switch (epi_mode) {                                                                                        \
+    case kEpiF32: return launch_gemm_t<NS_, kEpiF32>(g, nib, sc, colscale, at, rows, e, ws, st);             \
+    case kEpiTiled: return launch_gemm_t<NS_, kEpiTiled>(g, nib, sc, colscale, at, rows, e, ws, st);         \
+    default: return launch_gemm_t<NS_, kEpiHeadMajor>(g, nib, sc, colscale, at, rows, e, ws, st);            \
   }
-  return epi_mode == kEpiF32 ? launch_gemm_t<1, kEpiF32>(g, nib, sc, colscale, at, rows, e, decode, st)
-                             : launch_gemm_t<1, kEpiTiled>(g, nib, sc, colscale, at, rows, e, decode, st);
+  if (ns == 2) WQ4_GEMM(2);
+  WQ4_GEMM(1);
+#undef WQ4_GEMM
 }
 
 }  // namespace wq4

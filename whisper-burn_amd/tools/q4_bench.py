@@ -3,8 +3,9 @@
     python whisper-burn_amd/tools/q4_bench.py [--json out.json] [--iters 20]
 
 Times wq4_linear_forward_tiled (the GEMM alone, activations already in the
-A-tiled operand layout, as the model path feeds it) on torch's current HIP
-stream, and reports TFLOP/s and algorithmic GB/s against the MI355X peaks
+A-tiled operand layout, as the model path feeds it), captured `iters` times
+into one HIP graph on a side stream so small-M launches are not hidden by
+Python call overhead (--no-graph: plain back-to-back launches), and reports TFLOP/s and algorithmic GB/s against the MI355X peaks
 (2.5 PF dense f16/bf16 MFMA, 8.0 TB/s HBM; MI355X_MICROARCH.md:36,43).
 """
 from __future__ import annotations
@@ -38,31 +39,46 @@ def rand_q4(n: int, k: int, seed: int) -> np.ndarray:
     return blk.ravel()
 
 
-def bench_shape(torch, m: int, n: int, k: int, prec: int, policy: int, iters: int, warmup: int = 3) -> dict:
+def bench_shape(torch, m: int, n: int, k: int, prec: int, policy: int, iters: int, warmup: int = 3,
+                graph: bool = True) -> dict:
     L = wq4.lib()
     t = wq4.Q4Tensor.from_q4_bytes(rand_q4(n, k, n * 31 + k), [n, k])
     x = torch.randn((m, k), device="cuda:0", dtype=torch.float32)
     atb = L.wq4_atiled_bytes(m, k, prec)
     at = torch.empty(atb, dtype=torch.uint8, device="cuda:0")
     y = torch.empty((m, n), device="cuda:0", dtype=torch.float32)
-    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    wq4.check(L.wq4_tile_activations(ctypes.c_void_p(x.data_ptr()), m, k, k, prec, ctypes.c_void_p(at.data_ptr()),
-                                     atb, st))
-    wq4.set_kernel_policy(policy)
-
-    def run():
-        wq4.check(L.wq4_linear_forward_tiled(t.handle, None, ctypes.c_void_p(at.data_ptr()), None,
-                                             ctypes.c_void_p(y.data_ptr()), m, 0, prec, st))
-
-    for _ in range(warmup):
-        run()
+    side = torch.cuda.Stream()
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        run()
-    e1.record()
-    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        st = ctypes.c_void_p(side.cuda_stream)
+        wq4.check(L.wq4_tile_activations(ctypes.c_void_p(x.data_ptr()), m, k, k, prec,
+                                         ctypes.c_void_p(at.data_ptr()), atb, st))
+        wq4.set_kernel_policy(policy)
+
+        def run():
+            wq4.check(L.wq4_linear_forward_tiled(t.handle, None, ctypes.c_void_p(at.data_ptr()), None,
+                                                 ctypes.c_void_p(y.data_ptr()), m, 0, prec, st))
+
+        for _ in range(warmup):
+            run()
+        side.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if graph:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side):
+                for _ in range(iters):
+                    run()
+            g.replay()
+            side.synchronize()
+            e0.record(side)
+            g.replay()
+            e1.record(side)
+        else:
+            e0.record(side)
+            for _ in range(iters):
+                run()
+            e1.record(side)
+        side.synchronize()
     ms = e0.elapsed_time(e1) / iters
     wq4.set_kernel_policy(0)
     flops = 2.0 * m * n * k
@@ -78,17 +94,19 @@ def main() -> None:
     ap.add_argument("--json", default=None)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--decode-only", action="store_true")
     args = ap.parse_args()
     import torch
 
     rows = []
     enc_m = [1500, 48000] if not args.quick else [1500, 12000]
     for prec in (wq4.PREC_F16X2, wq4.PREC_F16):
-        for (n, k) in [(1280, 1280), (5120, 1280), (1280, 5120)]:
-            for m in enc_m:
-                rows.append(bench_shape(torch, m, n, k, prec, 1, args.iters))
-            for m in (1, 32, 128):
-                rows.append(bench_shape(torch, m, n, k, prec, 2, args.iters))
+        for (n, k) in [(1280, 1280), (3840, 1280), (5120, 1280), (1280, 5120)]:
+            for m in ([] if args.decode_only else enc_m):
+                rows.append(bench_shape(torch, m, n, k, prec, 1, args.iters, graph=not args.no_graph))
+            for m in (1, 32, 64):
+                rows.append(bench_shape(torch, m, n, k, prec, 2, args.iters, graph=not args.no_graph))
     for r in rows:
         print(f"{r['kernel']:8s} {r['prec']:6s} M={r['m']:6d} N={r['n']:5d} K={r['k']:5d}  {r['us']:9.1f} us  "
               f"{r['tflops']:7.1f} TF/s ({100 * r['frac_mfma']:5.1f}% MFMA)  {r['gbs']:7.0f} GB/s "
