@@ -13,9 +13,12 @@ the 256-clip / 8-GPU job); each rank runs its own clips (weak scaling, no
 collective on the data path -- one process per GPU, independent replicas).
 value = audio seconds of all ranks' clips / max-over-ranks wall seconds.
 
-roofline: the Q4 GEMMs (the north-star kernel, MFMA tile kernel), timed live
-with HIP events on their launch stream during the timed steps; algorithmic
-FLOPs = 2*M*N*K per launch.  cpu_baseline: the reference's CPU dequant->GEMM
+roofline: the dominant kernel by time per step -- the Q4 GEMMs (north-star
+kernel, MFMA tile kernel, timed live with HIP events on their launch stream
+during the timed steps; algorithmic FLOPs = 2*M*N*K per launch) or the decode
+step's cross-attention (HBM stream of the cached K/V; HIP-event timed by
+wa_probe_kernels right after the timed steps; algorithmic bytes = K + V of
+every clip).  Both, and the decode-step fc1 GEMM, are reported.  cpu_baseline: the reference's CPU dequant->GEMM
 path (src/gguf/tests.rs:60-87,172-184, restated in oracle/q4_oracle.c), one
 core, on one Large-V3 encoder layer's Q4 GEMMs at --cpu-rows rows, scaled to
 a clip's Q4 GEMM FLOPs (a lower bound on the CPU's per-clip time).
@@ -45,6 +48,45 @@ def clip_q4_gflop(cfg: dict, tokens: float) -> float:
     cross = cfg["n_text_layer"] * 2 * T * 2 * Dt * D
     per_tok = cfg["n_text_layer"] * 2 * (6 * Dt * Dt + 2 * 4 * Dt * Dt)
     return (enc + cross + per_tok * (4 + tokens)) * 1e-9
+
+
+def clip_ids(rank: int, B: int, warmup: int, steps: int) -> list[list[int]]:
+    """Global clip index of every clip a rank runs, per step (warmup first).
+    Ranks own disjoint contiguous ranges: independent clips, no exchange."""
+    per_rank = (warmup + steps) * B
+    return [[rank * per_rank + s * B + i for i in range(B)] for s in range(warmup + steps)]
+
+
+def max_over_ranks(x: float, dist, device) -> float:
+    """The job's wall time: max of the ranks' timed-region seconds (the only
+    collective in the run; not on the data path)."""
+    if dist is None:
+        return x
+    import torch
+
+    t = torch.tensor([x], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_rtf(world: int, B: int, steps: int, elapsed: float) -> float:
+    """Whole-job real-time factor: audio seconds of all ranks' clips / wall s."""
+    return world * B * steps * CLIP_SECONDS / elapsed
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, written by scripts/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per MI355X_MICROARCH.md
+    'HBM'), or None when absent."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    v = d.get("kernels", {}).get(kernel)
+    return None if v is None else v.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(cfg: dict, rows: int, tokens: float) -> dict:
@@ -114,12 +156,11 @@ def main() -> None:
     B = args.clips_per_gpu
     n_mels = cfg["n_mels"]
 
-    def batch(s: int):
-        base = 0x5EED0000 + (rank * (args.warmup + args.steps) + s) * B
-        arr = np.stack([whisper_amd.synth_uniform(base + i, "mel", n_mels * 3000, -1.5, 1.0) for i in range(B)])
-        return torch.from_numpy(arr.reshape(B, n_mels, 3000)).to(f"cuda:{local_rank}")
+    def batch(ids: list[int]):
+        arr = np.stack([whisper_amd.synth_uniform(0x5EED0000 + c, "mel", n_mels * 3000, -1.5, 1.0) for c in ids])
+        return torch.from_numpy(arr.reshape(len(ids), n_mels, 3000)).to(f"cuda:{local_rank}")
 
-    mels = [batch(s) for s in range(args.warmup + args.steps)]  # resident in HBM before timing
+    mels = [batch(ids) for ids in clip_ids(rank, B, args.warmup, args.steps)]  # resident in HBM before timing
     lang = None if args.lang < 0 else args.lang
     for s in range(args.warmup):
         model.transcribe(mels[s], lang, args.max_tokens, eot_stop=not args.fixed_length)
@@ -141,17 +182,38 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     model.profile_enable(False)
     prof = model.profile_read(reset=True)
-    if dist:
-        tt = torch.tensor([elapsed], device=f"cuda:{local_rank}", dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(elapsed, dist, f"cuda:{local_rank}")
     clips = world * B * args.steps
-    value = clips * CLIP_SECONDS / elapsed
+    value = job_rtf(world, B, args.steps, elapsed)
 
+    probe = model.probe_kernels(B, iters=20) if rank == 0 else None
     if rank == 0:
         q4 = prof["q4_gemm"]
-        achieved = q4["gflop"] / (q4["ms"] * 1e-3) * 1e-3 if q4["ms"] > 0 else 0.0
         mean_tok = float(np.mean(ntok)) if ntok else 0.0
+        steps_run = float(np.mean([t["steps"] for t in timings])) if timings else 0.0
+        # north-star kernel: the Q4 MFMA tile GEMMs (encoder + cross-K/V), timed live per launch
+        q4_tf = q4["gflop"] / (q4["ms"] * 1e-3) * 1e-3 if q4["ms"] > 0 else 0.0
+        roof_q4 = {"bound": "mfma", "achieved": round(q4_tf, 2), "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s",
+                   "frac": round(q4_tf / PEAK_MFMA_TFLOPS, 4),
+                   "traffic": pmc_traffic("q4_gemm_prefill_kernel"),
+                   "kernel": "q4_gemm_prefill_kernel (encoder + cross-K/V Q4 GEMMs)",
+                   "launches": q4["launches"], "avg_us": round(q4["ms"] / max(1, q4["launches"]) * 1e3, 2),
+                   "total_ms_per_step": round(q4["ms"] / args.steps, 2)}
+        # decode phase: cross-attention (HBM stream of the cached K/V), probed after the timed steps
+        xa = probe["cross_attention"]
+        xa_gbs = xa["bytes"] / (xa["us"] * 1e-6) * 1e-9
+        roof_xa = {"bound": "hbm", "achieved": round(xa_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                   "frac": round(xa_gbs / PEAK_HBM_GBS, 4), "traffic": pmc_traffic("cross_attn_kernel"),
+                   "kernel": "cross_attn_kernel (decode step, Tq = 1)", "avg_us": round(xa["us"], 2),
+                   "bytes_per_launch": xa["bytes"],
+                   "total_ms_per_step": round(xa["us"] * 1e-3 * cfg["n_text_layer"] * steps_run, 2)}
+        dq = probe["decode_fc1"]
+        roof_dq = {"bound": "hbm", "achieved": round(dq["bytes"] / (dq["us"] * 1e-6) * 1e-9, 1),
+                   "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                   "frac": round(dq["bytes"] / (dq["us"] * 1e-6) * 1e-9 / PEAK_HBM_GBS, 4), "traffic": None,
+                   "kernel": "q4_gemm_decode_kernel (decode-step fc1, split-K)", "avg_us": round(dq["us"], 2),
+                   "tflops": round(dq["flops"] / (dq["us"] * 1e-6) * 1e-12, 2)}
+        dominant = roof_xa if roof_xa["total_ms_per_step"] > roof_q4["total_ms_per_step"] else roof_q4
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "audio-s/wall-s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -163,10 +225,10 @@ def main() -> None:
                        "model": f"whisper-{args.variant.replace('_', '-')}-q4_0 (synthetic weights)",
                        "global_batch": clips // args.steps, "seq_len": cfg["n_audio_ctx"],
                        "parallelism": f"replicas{world} (independent clips, no collectives)"},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_MFMA_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_MFMA_TFLOPS, 4), "traffic": None,
-                         "kernel": "q4_gemm_prefill_kernel (encoder + cross-K/V Q4 GEMMs)",
-                         "launches": q4["launches"], "avg_us": round(q4["ms"] / max(1, q4["launches"]) * 1e3, 2)},
+            "roofline": dominant,
+            "roofline_q4_gemm": roof_q4,
+            "roofline_cross_attention": roof_xa,
+            "roofline_decode_gemm": roof_dq,
             "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
                             "tflops": round(v["gflop"] / (v["ms"] * 1e-3) * 1e-3, 2) if v["ms"] else None,
                             "gbs": round(v["gb"] / (v["ms"] * 1e-3), 1) if v["ms"] else None}

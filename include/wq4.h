@@ -71,10 +71,12 @@ wq4_precision wq4_get_precision(void);
 /* Q4Tensor::from_q4_bytes (tensor.rs:35-71).  `raw` = host bytes exactly as
  * stored in GGUF: N*K/32 blocks of 18 B (f16 scale LE, 16 nibble bytes; low
  * nibble = elements 0..15, high = 16..31).  Errors: WQ4_ESHAPE if N*K % 32
- * (tensor.rs:38-42) or, additionally to the reference, K % 32 (the shader
- * needs it, shader.wgsl:69, but Q4Tensor never checks); WQ4_EBYTES if nbytes
- * != N*K/32*18 (tensor.rs:43-48).  The bytes are repacked on upload into the
- * MFMA fragment order (lossless; wq4_tensor_raw_bytes returns them again). */
+ * (tensor.rs:38-42); WQ4_EBYTES if nbytes != N*K/32*18 (tensor.rs:43-48).
+ * The bytes are repacked on upload into the MFMA fragment order (lossless;
+ * wq4_tensor_raw_bytes returns them again).  Like Q4Tensor, a tensor whose
+ * K % 32 != 0 (blocks straddle rows) is accepted and can be dequantized, but
+ * every GEMM entry point rejects it with WQ4_ESHAPE (the shader needs whole
+ * blocks per row, shader.wgsl:69). */
 wq4_status wq4_tensor_create(int device, const uint8_t* raw, size_t nbytes, int64_t n, int64_t k,
                              wq4_tensor** out);
 void wq4_tensor_destroy(wq4_tensor* t);

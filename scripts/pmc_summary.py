@@ -1,0 +1,54 @@
+"""Summarise rocprofv3 PMC passes into profiles/pmc_traffic.json (bench.py roofline.traffic).
+
+    python scripts/pmc_summary.py ROUND   (reads gpurun_out/pmc_{FETCH_SIZE,WRITE_SIZE}_ROUND)
+
+HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950
+FETCH_SIZE reports half the bytes of a 16-B-per-lane streaming read and
+WRITE_SIZE the exact bytes of 16-B / dword stores (MI355X_MICROARCH.md, HBM).
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+FAMILIES = {"q4_gemm_prefill_kernel": r"q4_gemm_prefill_kernel", "q4_gemm_decode_kernel": r"q4_gemm_decode_kernel",
+            "cross_attn_kernel": r"cross_attn_kernel<2, 1>|cross_attn_kernelILi2ELi1E"}
+
+
+def load(counter: str, rnd: str) -> dict:
+    files = glob.glob(f"gpurun_out/pmc_{counter}_{rnd}/**/*counter_collection*.csv", recursive=True)
+    per = {}
+    for fn in files:
+        for row in csv.DictReader(open(fn)):
+            name, cname = row.get("Kernel_Name", ""), row.get("Counter_Name", "")
+            if cname != counter:
+                continue
+            for fam, rx in FAMILIES.items():
+                if re.search(rx, name):
+                    per.setdefault(fam, []).append(float(row["Counter_Value"]))
+    return per
+
+
+def main() -> None:
+    rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    fetch, write = load("FETCH_SIZE", rnd), load("WRITE_SIZE", rnd)
+    out = {"round": rnd, "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; "
+                                   "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch",
+           "kernels": {}}
+    for fam in FAMILIES:
+        f, w = fetch.get(fam, []), write.get(fam, [])
+        if not f or not w:
+            continue
+        fk, wk = sum(f) / len(f), sum(w) / len(w)
+        out["kernels"][fam] = {"launches_fetch": len(f), "launches_write": len(w), "fetch_size_kib": fk,
+                               "write_size_kib": wk, "hbm_bytes_per_launch": (2 * fk + wk) * 1024}
+    os.makedirs("profiles", exist_ok=True)
+    with open("profiles/pmc_traffic.json", "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -777,4 +777,47 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
   return WQ4_OK;
 }
 
+wq4_status wa_probe_kernels(wa_model* m, int n_clips, int iters, double* out) {
+  if (!m || !out) return fail(WQ4_EINVAL, "null argument");
+  if (n_clips < 1 || n_clips > m->bmax || iters < 1) return fail(WQ4_EINVAL, "bad n_clips / iters");
+  WA_HIP(hipSetDevice(m->device));
+  hipStream_t st = m->own_stream;
+  const Config& c = m->cfg;
+  const int B = n_clips, D = c.n_text_state, T = c.n_audio_ctx;
+  DecLayer& L = m->dec[0];
+  hipEvent_t a, b;
+  WA_HIP(hipEventCreate(&a));
+  WA_HIP(hipEventCreate(&b));
+  float ms = 0.0f;
+  // cross-attention of one decode step (Tq = 1): reads K and V of every clip
+  WA_HIP(wa::launch_cross_attention(m->qd, L.cross_kv, B, 1, T, c.n_text_head, m->xattn_part, m->xattn_counters,
+                                    m->atd_dec, m->ns, st));
+  WA_HIP(hipEventRecord(a, st));
+  for (int i = 0; i < iters; ++i)
+    WA_HIP(wa::launch_cross_attention(m->qd, L.cross_kv, B, 1, T, c.n_text_head, m->xattn_part, m->xattn_counters,
+                                      m->atd_dec, m->ns, st));
+  WA_HIP(hipEventRecord(b, st));
+  WA_HIP(hipEventSynchronize(b));
+  WA_HIP(hipEventElapsedTime(&ms, a, b));
+  out[0] = ms * 1e3 / iters;
+  out[1] = (double)B * T * 2 * D * 4 + (double)B * D * (4 + 2 * m->ns);
+  // fc1 of one decode step (M = n_clips rows, split-K decode kernel, tiled out)
+  const int F = 4 * D;
+  WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, m->atd_dec, nullptr, nullptr, m->atf_dec, B, WQ4_EPI_GELU | WQ4_EPI_TILED_OUT,
+                        m->prec, 2, st));
+  WA_HIP(hipEventRecord(a, st));
+  for (int i = 0; i < iters; ++i)
+    WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, m->atd_dec, nullptr, nullptr, m->atf_dec, B,
+                          WQ4_EPI_GELU | WQ4_EPI_TILED_OUT, m->prec, 2, st));
+  WA_HIP(hipEventRecord(b, st));
+  WA_HIP(hipEventSynchronize(b));
+  WA_HIP(hipEventElapsedTime(&ms, a, b));
+  out[2] = ms * 1e3 / iters;
+  out[3] = (double)F * D * 18 / 32 + (double)B * D * 2 * m->ns + (double)B * F * 2 * m->ns;
+  out[4] = 2.0 * B * F * D;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  return WQ4_OK;
+}
+
 }  // extern "C"

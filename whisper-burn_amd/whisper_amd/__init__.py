@@ -46,8 +46,9 @@ def lib() -> ctypes.CDLL:
         L.wa_synth_uniform.argtypes = [ctypes.c_uint64, ctypes.c_char_p, c_i64, ctypes.c_float, ctypes.c_float, f32p]
         L.wa_profile_enable.argtypes = [vp, c_int]
         L.wa_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), c_int]
+        L.wa_probe_kernels.argtypes = [vp, c_int, c_int, ctypes.POINTER(ctypes.c_double)]
         for n in ("wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
-                  "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read"):
+                  "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read", "wa_probe_kernels"):
             getattr(L, n).restype = c_int
         _lib = L
     return _lib
@@ -123,6 +124,13 @@ class WhisperModel:
         check(lib().wa_profile_read(self._h, buf, 1 if reset else 0))
         return {n: {"launches": int(buf[4 * i]), "ms": buf[4 * i + 1], "gflop": buf[4 * i + 2], "gb": buf[4 * i + 3]}
                 for i, n in enumerate(self.PROF_NAMES)}
+
+    def probe_kernels(self, n_clips: int, iters: int = 20) -> dict:
+        """HIP-event timing of single decode-step kernels (after transcribe)."""
+        buf = (ctypes.c_double * 5)()
+        check(lib().wa_probe_kernels(self._h, n_clips, iters, buf))
+        return {"cross_attention": {"us": buf[0], "bytes": buf[1]},
+                "decode_fc1": {"us": buf[2], "bytes": buf[3], "flops": buf[4]}}
 
     def encode(self, mel):
         """encoder.rs:87-115 -> encoder_out [B, 1500, D] (also fills the cross-K/V caches)."""
