@@ -16,6 +16,7 @@
 #include <cfloat>
 
 #include "../wq4_device.hpp"
+#include "../wq4_lnmath.hpp"
 #include "wa_kernels.hpp"
 
 namespace wa {
@@ -26,11 +27,9 @@ using wq4::half8;
 
 constexpr int kEOT = 50257;
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+using wq4::kLnMaxV;
+using wq4::wave_sum;
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -71,8 +70,7 @@ __host__ __device__ inline int kbp_of(int k) { return ((k / 32 + 1) / 2) * 2; }
 
 // ------------------------------------------------------------------ LN --
 // One wave per row; the row stays in registers (D <= 64 * 4 * kLnMaxV).
-constexpr int kLnMaxV = 8;
-
+// Arithmetic in wq4_lnmath.hpp, shared with the LN-fused decode GEMM.
 template <int NS, bool TILED>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ bb, int M, int D,
@@ -89,27 +87,13 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   }
   const float* xr = x + (size_t)row * D;
   floatx4 v[kLnMaxV];
-  float s = 0.0f;
 #pragma unroll
   for (int i = 0; i < kLnMaxV; ++i) {
     const int k = lane * 4 + 256 * i;
     v[i] = k < D ? *reinterpret_cast<const floatx4*>(xr + k) : floatx4{0.f, 0.f, 0.f, 0.f};
-    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
   }
-  const float mean = wave_sum(s) / (float)D;
-  float s2 = 0.0f;
-#pragma unroll
-  for (int i = 0; i < kLnMaxV; ++i) {
-    const int k = lane * 4 + 256 * i;
-    if (k < D) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float c = v[i][j] - mean;
-        s2 += c * c;
-      }
-    }
-  }
-  const float den = sqrtf(wave_sum(s2) / (float)D + 1e-5f);
+  float mean, den;
+  wq4::ln_row_stats(v, D, lane, mean, den);
 #pragma unroll
   for (int i = 0; i < kLnMaxV; ++i) {
     const int k = lane * 4 + 256 * i;
@@ -118,7 +102,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
       const floatx4 be = *reinterpret_cast<const floatx4*>(bb + k);
       float y[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) y[j] = ((v[i][j] - mean) / den) * g[j] + be[j];
+      for (int j = 0; j < 4; ++j) y[j] = wq4::ln_apply(v[i][j], mean, den, g[j], be[j]);
       if constexpr (TILED)
         atile_store4<NS>(tiled, row, k, kbp, y[0], y[1], y[2], y[3]);
       else
@@ -255,64 +239,167 @@ hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Floa
   return hipGetLastError();
 }
 
+// ---------------------------------------------- decode-step attention --
+// Shared by self- and cross-attention of the decoder (Tq <= 4 queries per
+// clip): 16 lanes share one key (4 dims each), 4 keys per load instruction,
+// U instructions in flight per wave, online softmax per 16-lane group, then a
+// fixed-order merge over the groups of a wave and over the 4 waves.
+
+// Online-softmax scan of keys [k0, k1).  rows(j, kp, vp) yields this lane's
+// 4-float K / V pointers of key j; vis(t, j) says whether query t sees key j.
+template <int TQ, int U, class Rows, class Vis>
+__device__ __forceinline__ void attn_scan(const floatx4 (&qv)[TQ], int Tq, int k0, int k1, int grp, Rows rows,
+                                          Vis vis, float (&m)[TQ], float (&l)[TQ], floatx4 (&o)[TQ]) {
+#pragma unroll
+  for (int t = 0; t < TQ; ++t) {
+    m[t] = -INFINITY;
+    l[t] = 0.0f;
+    o[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int j0 = k0; j0 < k1; j0 += 4 * U) {
+    floatx4 kk[U], vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = min(j0 + 4 * u + grp, k1 - 1);  // clamped: loads never branch
+      const float *kp, *vp;
+      rows(j, kp, vp);
+      kk[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(kp));
+      vv[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(vp));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + 4 * u + grp;
+#pragma unroll
+      for (int t = 0; t < TQ; ++t) {
+        if (t < Tq) {
+          float dot = qv[t][0] * kk[u][0] + qv[t][1] * kk[u][1] + qv[t][2] * kk[u][2] + qv[t][3] * kk[u][3];
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1) dot += __shfl_xor(dot, off, 64);
+          if (j < k1 && vis(t, j)) {
+            const float mn = fmaxf(m[t], dot);
+            const float alpha = expf(m[t] - mn);
+            const float p = expf(dot - mn);
+            l[t] = l[t] * alpha + p;
+            o[t] = o[t] * alpha + vv[u] * p;
+            m[t] = mn;
+          }
+        }
+      }
+    }
+  }
+}
+
+// Merge the 4 groups of each wave, then the 4 waves, in a fixed order.  Wave
+// t (< Tq) returns query t's (mn, ls, os = unnormalised o[lane]).
+template <int TQ>
+__device__ __forceinline__ void attn_merge(int Tq, int wave, int lane, float (&m)[TQ], float (&l)[TQ],
+                                           floatx4 (&o)[TQ], float (&wm)[4][TQ], float (&wl)[4][TQ],
+                                           float (&wo)[4][TQ][64], float& mn, float& ls, float& os) {
+  const int sub = lane & 15, grp = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < TQ; ++t) {
+    if (t >= Tq) break;
+#pragma unroll
+    for (int off = 16; off < 64; off <<= 1) {
+      const float m2 = __shfl_xor(m[t], off, 64), l2 = __shfl_xor(l[t], off, 64);
+      floatx4 o2;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o2[e] = __shfl_xor(o[t][e], off, 64);
+      const float mx = fmaxf(m[t], m2);
+      const float a1 = m[t] == -INFINITY ? 0.0f : expf(m[t] - mx);
+      const float a2 = m2 == -INFINITY ? 0.0f : expf(m2 - mx);
+      l[t] = l[t] * a1 + l2 * a2;
+      o[t] = o[t] * a1 + o2 * a2;
+      m[t] = mx;
+    }
+    if (grp == 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wo[wave][t][sub * 4 + e] = o[t][e];
+    }
+    if (lane == 0) {
+      wm[wave][t] = m[t];
+      wl[wave][t] = l[t];
+    }
+  }
+  __syncthreads();
+  mn = -INFINITY;
+  ls = 0.0f;
+  os = 0.0f;
+  if (wave < Tq) {
+    const int t = wave;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) mn = fmaxf(mn, wm[w][t]);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float a = wm[w][t] == -INFINITY ? 0.0f : expf(wm[w][t] - mn);
+      ls += wl[w][t] * a;
+      os += wo[w][t][lane] * a;
+    }
+  }
+}
+
 // ------------------------------------------ decoder self-attention --
-// One workgroup per (head, clip); wave t handles new token t (Tq <= 4).
-// Keys: the KV cache entries 0 .. kv_len + t (causal inside the new tokens).
+// One workgroup per (head, clip); the 4 waves split the keys 0 .. kv_len +
+// Tq - 1 (causal inside the new tokens).  Self-K/V caches are head-major
+// [clip][head][ctx][64] (contiguous per (clip, head)); the Tq new keys are
+// appended there for later steps and read here straight from the qkv rows.
 constexpr int kMaxCtx = 448;
 
-template <int NS>
+template <int NS, int TQ>
 __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restrict__ qkv, float* __restrict__ ck,
-                                                            float* __restrict__ cv, int Tq, int H, int ctx,
+                                                            float* __restrict__ cv, int Tq_, int H, int ctx,
                                                             const DecodeState* state, int kv_len_host,
                                                             _Float16* __restrict__ tiled) {
-  __shared__ float qs[4][64];
-  __shared__ float ps[4][kMaxCtx];
+  const int Tq = TQ == 1 ? 1 : Tq_;
+  __shared__ float wm[4][TQ], wl[4][TQ];
+  __shared__ float wo[4][TQ][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int head = blockIdx.x, b = blockIdx.y;
   const int D = H * 64;
+  const int sub = lane & 15, grp = lane >> 4;
   const int kv_len = state ? state->kv_len : kv_len_host;
+  const size_t hb = ((size_t)b * H + head) * ctx * 64;
   // append the new keys / values (decoder.rs:77-112 via Tensor::cat)
-  for (int idx = tid; idx < Tq * 64; idx += 256) {
-    const int t = idx >> 6, d = idx & 63;
-    const float* src = qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + d;
-    const size_t dst = ((size_t)b * ctx + kv_len + t) * D + head * 64 + d;
-    ck[dst] = src[D];
-    cv[dst] = src[2 * D];
-    qs[t][d] = src[0] * 0.125f;
+  if (tid < Tq * 16) {
+    const int t = tid >> 4, s4 = (tid & 15) * 4;
+    const float* src = qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + s4;
+    *reinterpret_cast<floatx4*>(ck + hb + (size_t)(kv_len + t) * 64 + s4) = *reinterpret_cast<const floatx4*>(src + D);
+    *reinterpret_cast<floatx4*>(cv + hb + (size_t)(kv_len + t) * 64 + s4) =
+        *reinterpret_cast<const floatx4*>(src + 2 * D);
   }
-  __syncthreads();
+  floatx4 qv[TQ];
+#pragma unroll
+  for (int t = 0; t < TQ; ++t)
+    qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + sub * 4) *
+                         0.125f
+                   : floatx4{0.f, 0.f, 0.f, 0.f};
+  const int nk = kv_len + Tq;
+  const int per_wave = (nk + 3) / 4;
+  const int k0 = min(nk, wave * per_wave), k1 = min(nk, k0 + per_wave);
+  const float* kb = ck + hb + sub * 4;
+  const float* vb = cv + hb + sub * 4;
+  const float* newb = qkv + (size_t)b * Tq * 3 * D + D + head * 64 + sub * 4;
+  float m[TQ], l[TQ];
+  floatx4 o[TQ];
+  attn_scan<TQ, 8>(
+      qv, Tq, k0, k1, grp,
+      [&](int j, const float*& kp, const float*& vp) {
+        if (j < kv_len) {
+          kp = kb + (size_t)j * 64;
+          vp = vb + (size_t)j * 64;
+        } else {  // this step's own keys: not yet visible through the cache
+          kp = newb + (size_t)(j - kv_len) * 3 * D;
+          vp = kp + D;
+        }
+      },
+      [&](int t, int j) { return j <= kv_len + t; }, m, l, o);
+  float mn, ls, os;
+  attn_merge<TQ>(Tq, wave, lane, m, l, o, wm, wl, wo, mn, ls, os);
   if (wave < Tq) {
     const int t = wave;
-    const int nk = kv_len + t + 1;
-    const float* kb = ck + (size_t)b * ctx * D + head * 64;
-    const float* vb = cv + (size_t)b * ctx * D + head * 64;
-    float mx = -INFINITY;
-    for (int j = lane; j < nk; j += 64) {
-      const float* kr = kb + (size_t)j * D;
-      float dot = 0.0f;
-#pragma unroll
-      for (int d = 0; d < 64; d += 4) {
-        const floatx4 k4 = *reinterpret_cast<const floatx4*>(kr + d);
-        dot += qs[t][d] * k4[0] + qs[t][d + 1] * k4[1] + qs[t][d + 2] * k4[2] + qs[t][d + 3] * k4[3];
-      }
-      ps[t][j] = dot;
-      mx = fmaxf(mx, dot);
-    }
-    mx = wave_max(mx);
-    float sum = 0.0f;
-    for (int j = lane; j < nk; j += 64) {
-      const float p = expf(ps[t][j] - mx);
-      ps[t][j] = p;
-      sum += p;
-    }
-    sum = wave_sum(sum);
-    __builtin_amdgcn_wave_barrier();
-    float o = 0.0f;
-    for (int j = 0; j < nk; ++j) o += ps[t][j] * vb[(size_t)j * D + lane];
-    o = o / sum;
-    // lanes 4g..4g+3 hold d = 4g..4g+3 -> gather to lane 4g and store 4 halves
-    const float o1 = __shfl_down(o, 1, 64), o2 = __shfl_down(o, 2, 64), o3 = __shfl_down(o, 3, 64);
-    if ((lane & 3) == 0) atile_store4<NS>(tiled, b * Tq + t, head * 64 + lane, kbp_of(D), o, o1, o2, o3);
+    const float val = os / ls;
+    const float v1 = __shfl_down(val, 1, 64), v2 = __shfl_down(val, 2, 64), v3 = __shfl_down(val, 3, 64);
+    if ((lane & 3) == 0) atile_store4<NS>(tiled, b * Tq + t, head * 64 + lane, kbp_of(D), val, v1, v2, v3);
   }
 }
 
@@ -321,12 +408,15 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
                                          int ns, hipStream_t st) {
   if (Tq > 4 || ctx > kMaxCtx) return hipErrorInvalidValue;
   const dim3 grid(H, B), block(256);
-  if (ns == 2)
-    hipLaunchKernelGGL((dec_self_attn_kernel<2>), grid, block, 0, st, qkv, cache_k, cache_v, Tq, H, ctx, state,
-                       kv_len_host, tiled);
-  else
-    hipLaunchKernelGGL((dec_self_attn_kernel<1>), grid, block, 0, st, qkv, cache_k, cache_v, Tq, H, ctx, state,
-                       kv_len_host, tiled);
+#define WA_SELF(NS_, TQ_)                                                                                      \
+  hipLaunchKernelGGL((dec_self_attn_kernel<NS_, TQ_>), grid, block, 0, st, qkv, cache_k, cache_v, Tq, H, ctx, \
+                     state, kv_len_host, tiled)
+  if (ns == 2) {
+    if (Tq == 1) WA_SELF(2, 1); else WA_SELF(2, 4);
+  } else {
+    if (Tq == 1) WA_SELF(1, 1); else WA_SELF(1, 4);
+  }
+#undef WA_SELF
   return hipGetLastError();
 }
 
@@ -335,12 +425,9 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
 // layer and step).  Grid = (H * S, B): the T encoder keys of each (head,
 // clip) are split over S workgroups (S depends on T only -> batch
 // invariant) so the chip sees ~10 balanced workgroups per CU instead of 2-3
-// unbalanced ones.  Inside a workgroup 4 waves split the keys; 16 lanes share
-// one key (4 dims each), 4 keys per load instruction, U instructions in
-// flight, online softmax per 16-lane group, merged across groups and waves in
-// a fixed order.  With S > 1 each workgroup publishes (m, l, o[64]) per query
-// write-through (sc1); the last arriver of the (head, clip) merges the S
-// partials in split order (cdna_hip_programming.md Guideline 16, R1) and
+// unbalanced ones.  With S > 1 each workgroup publishes (m, l, o[64]) per
+// query write-through (sc1); the last arriver of the (head, clip) merges the
+// S partials in split order (cdna_hip_programming.md Guideline 16, R1) and
 // writes the A-tiled operand of the output projection.
 constexpr int kXattnMaxSplit = 8;
 constexpr int kXattnPart = 68;  // floats per (query) partial: o[64], m, l, pad
@@ -367,18 +454,8 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const float* __restrict
   floatx4 qv[TQ];
 #pragma unroll
   for (int t = 0; t < TQ; ++t)
-    qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(q + (size_t)(b * Tq + t) * D + head * 64 + sub * 4)
+    qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(q + (size_t)(b * Tq + t) * D + head * 64 + sub * 4) * 0.125f
                    : floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int t = 0; t < TQ; ++t) qv[t] = qv[t] * 0.125f;
-  float m[TQ], l[TQ];
-  floatx4 o[TQ];
-#pragma unroll
-  for (int t = 0; t < TQ; ++t) {
-    m[t] = -INFINITY;
-    l[t] = 0.0f;
-    o[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  }
   const int per_split = (T + S - 1) / S;
   const int s0 = split * per_split, s1 = min(T, s0 + per_split);
   const int per_wave = (s1 - s0 + 3) / 4;
@@ -386,77 +463,17 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const float* __restrict
   // head-major K / V: [2][B][H][T][64] (wq4_gemm_tiled_headmajor)
   const float* kb = kv + ((size_t)b * H + head) * T * 64 + sub * 4;
   const size_t vofs = (size_t)gridDim.y * H * T * 64;
-  constexpr int U = 8;  // 32 keys per wave in flight
-  for (int j0 = k0; j0 < k1; j0 += 4 * U) {
-    floatx4 kk[U], vv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = min(j0 + 4 * u + grp, k1 - 1);  // clamped: loads never branch
-      const float* r = kb + (size_t)j * 64;
-      kk[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(r));
-      vv[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(r + vofs));
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool ok = j0 + 4 * u + grp < k1;
-#pragma unroll
-      for (int t = 0; t < TQ; ++t) {
-        if (t < Tq) {
-          float dot = qv[t][0] * kk[u][0] + qv[t][1] * kk[u][1] + qv[t][2] * kk[u][2] + qv[t][3] * kk[u][3];
-#pragma unroll
-          for (int off = 1; off < 16; off <<= 1) dot += __shfl_xor(dot, off, 64);
-          if (ok) {
-            const float mn = fmaxf(m[t], dot);
-            const float alpha = expf(m[t] - mn);
-            const float p = expf(dot - mn);
-            l[t] = l[t] * alpha + p;
-            o[t] = o[t] * alpha + vv[u] * p;
-            m[t] = mn;
-          }
-        }
-      }
-    }
-  }
-  // merge the 4 groups of the wave, then the 4 waves (fixed order)
-#pragma unroll
-  for (int t = 0; t < TQ; ++t) {
-    if (t >= Tq) break;
-#pragma unroll
-    for (int off = 16; off < 64; off <<= 1) {
-      const float m2 = __shfl_xor(m[t], off, 64), l2 = __shfl_xor(l[t], off, 64);
-      floatx4 o2;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o2[e] = __shfl_xor(o[t][e], off, 64);
-      const float mn = fmaxf(m[t], m2);
-      const float a1 = m[t] == -INFINITY ? 0.0f : expf(m[t] - mn);
-      const float a2 = m2 == -INFINITY ? 0.0f : expf(m2 - mn);
-      l[t] = l[t] * a1 + l2 * a2;
-      o[t] = o[t] * a1 + o2 * a2;
-      m[t] = mn;
-    }
-    if (grp == 0) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) wo[wave][t][sub * 4 + e] = o[t][e];
-    }
-    if (lane == 0) {
-      wm[wave][t] = m[t];
-      wl[wave][t] = l[t];
-    }
-  }
-  __syncthreads();
-  // wave t merges the 4 waves for query t: (mn, ls, os[lane])
-  float mn = -INFINITY, ls = 0.0f, os = 0.0f;
-  if (wave < Tq) {
-    const int t = wave;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) mn = fmaxf(mn, wm[w][t]);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const float a = wm[w][t] == -INFINITY ? 0.0f : expf(wm[w][t] - mn);
-      ls += wl[w][t] * a;
-      os += wo[w][t][lane] * a;
-    }
-  }
+  float m[TQ], l[TQ];
+  floatx4 o[TQ];
+  attn_scan<TQ, 8>(
+      qv, Tq, k0, k1, grp,
+      [&](int j, const float*& kp, const float*& vp) {
+        kp = kb + (size_t)j * 64;
+        vp = kp + vofs;
+      },
+      [](int, int) { return true; }, m, l, o);
+  float mn, ls, os;
+  attn_merge<TQ>(Tq, wave, lane, m, l, o, wm, wl, wo, mn, ls, os);
   if (S > 1) {
     typedef __attribute__((address_space(1))) float gfloat;
     typedef __attribute__((address_space(1))) int gint;
