@@ -154,6 +154,14 @@ wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void
                           float* y_dev, void* at_out_dev, int64_t rows, unsigned flags, wq4_precision prec,
                           int kernel, void* stream);
 
+/* LayerNorm (src/model/layers.rs:12-32: eps 1e-5, biased variance) of
+ * rows x d f32 rows, written either as the A-tiled operand of a following
+ * GEMM with K = d (at_out_dev, wq4_atiled_bytes(rows, d, prec) bytes) or as
+ * f32 rows (y_dev); exactly one of the two is non-NULL.  d % 4 == 0,
+ * d <= 2048. */
+wq4_status wq4_layernorm(const float* x_dev, const float* w_dev, const float* b_dev, int64_t rows, int64_t d,
+                         wq4_precision prec, void* at_out_dev, float* y_dev, void* stream);
+
 /* Fused K|V projection written head-major for attention: w is [parts * d, K]
  * (parts stacked projections of d = heads * 64 columns each), rows =
  * groups * group_rows; y_dev[part][group][head][t][64] (the [B, H, T, 64]

@@ -40,93 +40,10 @@ __device__ __forceinline__ floatx16 mfma_f32(float a, float b, const floatx16& c
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-// Index (in halves) of element (row, k) of an A-tiled operand with kbp
-// (even) Q4 blocks per row, split s.
-__device__ __forceinline__ size_t atile_index(int row, int k, int kbp, int ns, int s) {
-  const int mt = row >> 5, r = row & 31;
-  const int b = k >> 5, kk = (k >> 4) & 1, hh = (k >> 3) & 1, j = k & 7;
-  return (((((size_t)mt * kbp + b) * 2 + kk) * ns + s) * 64 + (r + 32 * hh)) * 8 + j;
-}
+using wq4::atile_store4;
+using wq4::kbp_of;
 
-// Write 4 consecutive k (k % 4 == 0) of one row into the A-tiled operand.
-template <int NS>
-__device__ __forceinline__ void atile_store4(_Float16* t, int row, int k, int kbp, float a, float b, float c,
-                                             float d) {
-  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-  half4 hi, lo;
-  const float v[4] = {a, b, c, d};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    _Float16 x, y;
-    wq4::split_f16(v[j], x, y);
-    hi[j] = x;
-    lo[j] = y;
-  }
-  *reinterpret_cast<half4*>(t + atile_index(row, k, kbp, NS, 0)) = hi;
-  if constexpr (NS == 2) *reinterpret_cast<half4*>(t + atile_index(row, k, kbp, NS, 1)) = lo;
-}
 
-__host__ __device__ inline int kbp_of(int k) { return ((k / 32 + 1) / 2) * 2; }
-
-// ------------------------------------------------------------------ LN --
-// One wave per row; the row stays in registers (D <= 64 * 4 * kLnMaxV).
-// Arithmetic in wq4_lnmath.hpp, shared with the LN-fused decode GEMM.
-template <int NS, bool TILED>
-__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                        const float* __restrict__ bb, int M, int D,
-                                                        _Float16* __restrict__ tiled, float* __restrict__ out) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int kbp = kbp_of(D);
-  const int rows_total = TILED ? ((M + 31) / 32) * 32 : M;
-  const int row = blockIdx.x * 4 + wave;
-  if (row >= rows_total) return;
-  if (row >= M) {  // padded rows of the last m-tile: finite zeros
-    if constexpr (TILED)
-      for (int k = lane * 4; k < D; k += 256) atile_store4<NS>(tiled, row, k, kbp, 0.f, 0.f, 0.f, 0.f);
-    return;
-  }
-  const float* xr = x + (size_t)row * D;
-  floatx4 v[kLnMaxV];
-#pragma unroll
-  for (int i = 0; i < kLnMaxV; ++i) {
-    const int k = lane * 4 + 256 * i;
-    v[i] = k < D ? *reinterpret_cast<const floatx4*>(xr + k) : floatx4{0.f, 0.f, 0.f, 0.f};
-  }
-  float mean, den;
-  wq4::ln_row_stats(v, D, lane, mean, den);
-#pragma unroll
-  for (int i = 0; i < kLnMaxV; ++i) {
-    const int k = lane * 4 + 256 * i;
-    if (k < D) {
-      const floatx4 g = *reinterpret_cast<const floatx4*>(w + k);
-      const floatx4 be = *reinterpret_cast<const floatx4*>(bb + k);
-      float y[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) y[j] = wq4::ln_apply(v[i][j], mean, den, g[j], be[j]);
-      if constexpr (TILED)
-        atile_store4<NS>(tiled, row, k, kbp, y[0], y[1], y[2], y[3]);
-      else
-        *reinterpret_cast<floatx4*>(out + (size_t)row * D + k) = floatx4{y[0], y[1], y[2], y[3]};
-    }
-  }
-}
-
-hipError_t launch_layernorm(const float* x, const float* w, const float* b, int M, int D, _Float16* tiled, int ns,
-                            float* out, hipStream_t st) {
-  if (M <= 0) return hipSuccess;
-  if (D % 4 != 0 || D > 256 * kLnMaxV) return hipErrorInvalidValue;
-  const int rows_total = tiled ? ((M + 31) / 32) * 32 : M;
-  const dim3 grid((rows_total + 3) / 4), block(256);
-  if (tiled) {
-    if (ns == 2)
-      hipLaunchKernelGGL((layernorm_kernel<2, true>), grid, block, 0, st, x, w, b, M, D, tiled, out);
-    else
-      hipLaunchKernelGGL((layernorm_kernel<1, true>), grid, block, 0, st, x, w, b, M, D, tiled, out);
-  } else {
-    hipLaunchKernelGGL((layernorm_kernel<2, false>), grid, block, 0, st, x, w, b, M, D, tiled, out);
-  }
-  return hipGetLastError();
-}
 
 // ------------------------------------------------- encoder attention --
 // One workgroup = 4 waves = 128 queries of one (clip, head); each wave owns

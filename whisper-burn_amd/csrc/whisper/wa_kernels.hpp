@@ -16,12 +16,6 @@ struct DecodeState {
   int n_done;    // clips that have emitted EOT
 };
 
-// LayerNorm (layers.rs:23-31, eps 1e-5, biased variance) of rows [M, D].
-// tiled != nullptr: write the A-tiled f16 operand (ns splits) of a Q4 GEMM;
-// else write f32 row-major `out` (ld = D).
-hipError_t launch_layernorm(const float* x, const float* w, const float* b, int M, int D, _Float16* tiled,
-                            int ns, float* out, hipStream_t st);
-
 // Encoder self-attention (attention.rs:243-298, non-causal), flash-style,
 // f32 MFMA.  qkv: [B*T, 3D] f32 (q | k | v).  Writes the A-tiled operand of
 // the output projection (rows b*T + t, K = D).

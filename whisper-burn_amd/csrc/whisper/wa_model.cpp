@@ -451,7 +451,7 @@ wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st,
   for (auto& L : m->enc) {  // EncoderBlock::forward (encoder.rs:37-49)
     {
       Prof p(m, st, 3, 0.0, ln_gb);
-      WA_HIP(wa::launch_layernorm(m->x, L.ln1_w, L.ln1_b, (int)rows, D, m->at_d, m->ns, nullptr, st));
+      WA_WQ4(wq4_layernorm(m->x, L.ln1_w, L.ln1_b, rows, D, m->prec, m->at_d, nullptr, st));
     }
     {
       Prof p = q4prof(m, st, L.qkv, rows);
@@ -467,7 +467,7 @@ wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st,
     }
     {
       Prof p(m, st, 3, 0.0, ln_gb);
-      WA_HIP(wa::launch_layernorm(m->x, L.ln2_w, L.ln2_b, (int)rows, D, m->at_d, m->ns, nullptr, st));
+      WA_WQ4(wq4_layernorm(m->x, L.ln2_w, L.ln2_b, rows, D, m->prec, m->at_d, nullptr, st));
     }
     {
       Prof p = q4prof(m, st, L.fc1, rows);
@@ -481,9 +481,9 @@ wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st,
   }
   {
     Prof p(m, st, 3, 0.0, ln_gb);
-    WA_HIP(wa::launch_layernorm(m->x, m->lnp_w, m->lnp_b, (int)rows, D, m->enc_at, m->ns, nullptr, st));
+    WA_WQ4(wq4_layernorm(m->x, m->lnp_w, m->lnp_b, rows, D, m->prec, m->enc_at, nullptr, st));
   }
-  if (enc_out_f32) WA_HIP(wa::launch_layernorm(m->x, m->lnp_w, m->lnp_b, (int)rows, D, nullptr, 2, enc_out_f32, st));
+  if (enc_out_f32) WA_WQ4(wq4_layernorm(m->x, m->lnp_w, m->lnp_b, rows, D, WQ4_PREC_F16X2, nullptr, enc_out_f32, st));
   return WQ4_OK;
 }
 
@@ -510,25 +510,25 @@ wq4_status decoder_forward(wa_model* m, const int* tokens, int B, int Tq, const 
   const int64_t rows = (int64_t)B * Tq;
   WA_HIP(wa::launch_embed(tokens, m->tok_emb, m->dec_pos, B, Tq, D, state, pos0, m->xd, st));
   for (auto& L : m->dec) {  // DecoderBlock (decoder.rs:77-112 / 140-183)
-    WA_HIP(wa::launch_layernorm(m->xd, L.ln1_w, L.ln1_b, (int)rows, D, m->atd_dec, m->ns, nullptr, st));
+    WA_WQ4(wq4_layernorm(m->xd, L.ln1_w, L.ln1_b, rows, D, m->prec, m->atd_dec, nullptr, st));
     WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, m->atd_dec, nullptr, m->qkvd, nullptr, rows, 0u, m->prec, 2, st));
     WA_HIP(wa::launch_decoder_self_attention(m->qkvd, L.cache_k, L.cache_v, B, Tq, H, c.n_text_ctx, state, kv0,
                                              m->atd_dec, m->ns, st));
     WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, m->atd_dec, m->xd, m->xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
-    WA_HIP(wa::launch_layernorm(m->xd, L.ln2_w, L.ln2_b, (int)rows, D, m->atd_dec, m->ns, nullptr, st));
+    WA_WQ4(wq4_layernorm(m->xd, L.ln2_w, L.ln2_b, rows, D, m->prec, m->atd_dec, nullptr, st));
     WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, m->atd_dec, nullptr, m->qd, nullptr, rows, 0u, m->prec, 2, st));
     WA_HIP(wa::launch_cross_attention(m->qd, L.cross_kv, B, Tq, c.n_audio_ctx, H, m->xattn_part, m->xattn_counters,
                                       m->atd_dec, m->ns, st));
     WA_WQ4(wq4_gemm_tiled(L.cout, L.cout_b, m->atd_dec, m->xd, m->xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2,
                           st));
-    WA_HIP(wa::launch_layernorm(m->xd, L.ln3_w, L.ln3_b, (int)rows, D, m->atd_dec, m->ns, nullptr, st));
+    WA_WQ4(wq4_layernorm(m->xd, L.ln3_w, L.ln3_b, rows, D, m->prec, m->atd_dec, nullptr, st));
     WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, m->atd_dec, nullptr, nullptr, m->atf_dec, rows,
                           WQ4_EPI_GELU | WQ4_EPI_TILED_OUT, m->prec, 2, st));
     WA_WQ4(wq4_gemm_tiled(L.fc2, L.fc2_b, m->atf_dec, m->xd, m->xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
   }
   // final LN (decoder.rs:286 / 340) and tied-embedding logits of the last
   // position of every clip (decoder.rs:289-292, 342-343)
-  WA_HIP(wa::launch_layernorm(m->xd, m->dln_w, m->dln_b, (int)rows, D, nullptr, 2, m->hid, st));
+  WA_WQ4(wq4_layernorm(m->xd, m->dln_w, m->dln_b, rows, D, WQ4_PREC_F16X2, nullptr, m->hid, st));
   WA_HIP(wa::launch_logits(m->hid + (size_t)(Tq - 1) * D, B, D, (int64_t)Tq * D, m->tok_emb, c.n_vocab, m->logits,
                            st));
   return WQ4_OK;

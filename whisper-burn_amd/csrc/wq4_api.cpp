@@ -541,6 +541,21 @@ wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void
               ns_of(prec), static_cast<hipStream_t>(stream), dec);
 }
 
+wq4_status wq4_layernorm(const float* x_dev, const float* w_dev, const float* b_dev, int64_t rows, int64_t d,
+                         wq4_precision prec, void* at_out_dev, float* y_dev, void* stream) {
+  wq4_status s = check_prec(prec);
+  if (s != WQ4_OK) return s;
+  if (!x_dev || !w_dev || !b_dev || (at_out_dev == nullptr) == (y_dev == nullptr))
+    return fail(WQ4_EINVAL, "layernorm needs x, w, b and exactly one of at_out / y");
+  if (rows < 0 || rows > (1 << 24) || d <= 0 || d % 4 != 0 || d > 2048)
+    return fail(WQ4_ESHAPE, "layernorm needs d % 4 == 0, d <= 2048");
+  if (rows == 0) return WQ4_OK;
+  hipError_t e = wq4::launch_layernorm(x_dev, w_dev, b_dev, (int)rows, (int)d, static_cast<_Float16*>(at_out_dev),
+                                       ns_of(prec), y_dev, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "layernorm launch");
+  return WQ4_OK;
+}
+
 wq4_status wq4_gemm_tiled_headmajor(const wq4_tensor* w, const float* bias_dev, const void* at_dev, float* y_dev,
                                     int64_t rows, int group_rows, int d, wq4_precision prec, int kernel,
                                     void* stream) {

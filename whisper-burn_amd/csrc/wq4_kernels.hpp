@@ -8,6 +8,11 @@
 
 namespace wq4 {
 
+// LayerNorm (layers.rs:12-32) of M rows of D: A-tiled f16 split operand
+// (tiled != null, ns = 1 or 2) or f32 rows (out).
+hipError_t launch_layernorm(const float* x, const float* w, const float* b, int M, int D, _Float16* tiled, int ns,
+                            float* out, hipStream_t st);
+
 // f32 [M, ld] row-major -> A-tiled f16 split (ns = 1 or 2).
 hipError_t launch_tile_activations(const float* x, _Float16* at, int M, int K, int ld, int ns, hipStream_t st);
 
@@ -15,7 +20,8 @@ hipError_t launch_tile_activations(const float* x, _Float16* at, int M, int K, i
 // tiles and per-n-tile arrival counters (zeroed once, re-armed by the kernel).
 constexpr int64_t kDecodeWsFloats = (int64_t)4 << 20;  // 16 MiB of partials
 constexpr int64_t kDecodeMaxTiles = 1 << 16;            // counters
-constexpr int kDecodeMaxPer = 4;                        // block pairs per wave
+constexpr int kDecodeMaxPer = 4;                        // block pairs per wave (4-wave split-K)
+constexpr int kDecodeMaxPer8 = 3;                       // block pairs per wave (8-wave, whole K)
 constexpr int kDecodeMaxMTiles = 4;                     // rows <= 128 (launches of 2 m-tiles)
 struct DecodeWs {
   float* part;
@@ -25,6 +31,7 @@ struct DecodePlan {
   int per;    // kernel instance: max block pairs per wave
   int ks;     // workgroups (K slices) per n-tile
   int chunk;  // block pairs per wave (<= per)
+  int w;      // waves per workgroup (4: split-K, 8: whole K per workgroup)
 };
 DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal);
 

@@ -1,6 +1,6 @@
-// wq4_lnmath.hpp -- LayerNorm arithmetic shared bit-for-bit by the model's
-// LayerNorm kernel (whisper/wa_kernels.hip) and the LN-fused decode GEMM
-// (wq4_q4gemm.hip): src/model/layers.rs:12-32 (eps 1e-5, biased variance,
+// wq4_lnmath.hpp -- LayerNorm arithmetic shared bit-for-bit by the
+// LayerNorm kernel (wq4_ln.hip) and the residual + LayerNorm tail of the
+// decode GEMM (wq4_q4gemm.hip), plus the A-tiled operand store helpers: src/model/layers.rs:12-32 (eps 1e-5, biased variance,
 // two-pass mean / variance).  One wave owns a row; lane l holds the float4s
 // at k = 4 l + 256 i.  Both kernels call exactly these functions, so the
 // fused and unfused decode paths produce identical operands.
@@ -40,6 +40,34 @@ __device__ __forceinline__ void ln_row_stats(const floatx4 (&v)[kLnMaxV], int D,
   }
   den = sqrtf(wave_sum(s2) / (float)D + 1e-5f);
 }
+
+// Index (in halves) of element (row, k) of an A-tiled operand with kbp
+// (even) Q4 blocks per row, split s.
+__device__ __forceinline__ size_t atile_index(int row, int k, int kbp, int ns, int s) {
+  const int mt = row >> 5, r = row & 31;
+  const int b = k >> 5, kk = (k >> 4) & 1, hh = (k >> 3) & 1, j = k & 7;
+  return (((((size_t)mt * kbp + b) * 2 + kk) * ns + s) * 64 + (r + 32 * hh)) * 8 + j;
+}
+
+// Write 4 consecutive k (k % 4 == 0) of one row into the A-tiled operand.
+template <int NS>
+__device__ __forceinline__ void atile_store4(_Float16* t, int row, int k, int kbp, float a, float b, float c,
+                                             float d) {
+  typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+  half4 hi, lo;
+  const float v[4] = {a, b, c, d};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    _Float16 x, y;
+    split_f16(v[j], x, y);
+    hi[j] = x;
+    lo[j] = y;
+  }
+  *reinterpret_cast<half4*>(t + atile_index(row, k, kbp, NS, 0)) = hi;
+  if constexpr (NS == 2) *reinterpret_cast<half4*>(t + atile_index(row, k, kbp, NS, 1)) = lo;
+}
+
+__host__ __device__ inline int kbp_of(int k) { return ((k / 32 + 1) / 2) * 2; }
 
 __device__ __forceinline__ float ln_apply(float v, float mean, float den, float g, float b) {
   return ((v - mean) / den) * g + b;

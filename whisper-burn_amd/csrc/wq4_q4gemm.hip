@@ -374,18 +374,18 @@ __device__ __forceinline__ void decode_epilogue(const floatx16& s, float cs, int
   }
 }
 
-template <int NS, int EPI, int PER, int MT>
-__global__ __launch_bounds__(256) void q4_gemm_decode_kernel(const uint8_t* __restrict__ nib,
+template <int NS, int EPI, int PER, int MT, int W>
+__global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* __restrict__ nib,
                                                               const uint32_t* __restrict__ sc,
                                                               const float* __restrict__ colscale,
                                                               const _Float16* __restrict__ at, int mt0, int nbp, int ks,
                                                               int chunk, float* __restrict__ part,
                                                               int* __restrict__ counters, EpiArgs e) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  constexpr int W = kDecodeWaves;
   constexpr int mtiles = MT;
-  float* red = reinterpret_cast<float*>(smem);                        // [W-1][16][64]
-  float* stage = reinterpret_cast<float*>(smem) + (W - 1) * 16 * 64;  // [32][kStageLd]
+  constexpr int kRedWaves = W == 8 ? W : W - 1;
+  float* red = reinterpret_cast<float*>(smem);                          // [kRedWaves][16][64]
+  float* stage = reinterpret_cast<float*>(smem) + kRedWaves * 16 * 64;  // [32][kStageLd]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar buffer descriptors
@@ -460,6 +460,75 @@ __global__ __launch_bounds__(256) void q4_gemm_decode_kernel(const uint8_t* __re
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = acc0[i] + acc1[i];
 
+    if constexpr (W == 8) {
+      // whole K in this workgroup: every wave finalises 2 of the 16
+      // accumulator registers (same wave-order sum as the 4-wave path) and
+      // applies their epilogue -- the reduction and epilogue run 8-wide
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[(wave * 16 + i) * 64 + lane] = acc[i];
+      __syncthreads();
+      const int h = lane >> 5;
+      const int col = nt * 32 + r;
+      float v[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = 2 * wave + q;
+        v[q] = red[i * 64 + lane];
+#pragma unroll
+        for (int w = 1; w < W; ++w) v[q] = v[q] + red[(w * 16 + i) * 64 + lane];
+      }
+      typedef __attribute__((address_space(1))) int gint;
+      gint* ctr = (gint*)(counters + nt);
+      if (ks > 1) {
+        // split-K: every wave publishes its 2 registers write-through (sc1),
+        // drains, and one lane takes the ticket; the slice drawing ks-1 sums
+        // the slabs in slice order (cdna_hip_programming.md Guideline 16, R1)
+        const __amdgpu_buffer_rsrc_t rs = brsrc(part + ((size_t)nt * ks + slice) * 1024, 4096);
+        const floatx2 f2 = {v[0], v[1]};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, f2), rs, (wave * 64 + lane) * 8, 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // every storing wave drained before the ticket; red[] free again
+        if (tid == 0) {
+          const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          red[0] = prev == ks - 1 ? 1.0f : 0.0f;
+        }
+        __syncthreads();
+        if (red[0] == 0.0f) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: loads stay below the ticket
+        const __amdgpu_buffer_rsrc_t ra = brsrc(part + (size_t)nt * ks * 1024, (uint32_t)ks * 4096);
+        u32x2 pv[kDecodeMaxKs];
+#pragma unroll
+        for (int sl = 0; sl < kDecodeMaxKs; ++sl)
+          pv[sl] = __builtin_amdgcn_raw_buffer_load_b64(ra, sl < ks ? sl * 4096 + (wave * 64 + lane) * 8 : kOob, 0,
+                                                        16);
+        floatx2 t = __builtin_bit_cast(floatx2, pv[0]);
+#pragma unroll
+        for (int sl = 1; sl < kDecodeMaxKs; ++sl)
+          if (sl < ks) t = t + __builtin_bit_cast(floatx2, pv[sl]);
+        v[0] = t[0];
+        v[1] = t[1];
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = 2 * wave + q;
+        const int rl = acc_row(i, h);
+        const int row = (mt0 + mt) * 32 + rl;
+        if constexpr (EPI == kEpiTiled) {
+          stage[rl * kStageLd + r] = (row < e.m && col < e.n) ? epi_value(v[q] * cs, row, col, e) : 0.0f;
+        } else {
+          if (row < e.m && col < e.n)
+            e.out[EPI == kEpiHeadMajor ? out_index(e, row, col) : (size_t)row * e.ldo + col] =
+                epi_value(v[q] * cs, row, col, e);
+        }
+      }
+      if constexpr (EPI == kEpiTiled) {
+        __syncthreads();
+        if (wave == 0) store_tiled_slab<NS, 1>(stage, e, mt0 + mt, nt, lane);
+      }
+      if (ks > 1 && tid == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+      continue;  // MT == 1 for 8-wave plans
+    }
+
     // fixed-order reduction over the W waves
     if (wave > 0) {
 #pragma unroll
@@ -472,7 +541,7 @@ __global__ __launch_bounds__(256) void q4_gemm_decode_kernel(const uint8_t* __re
       for (int w = 0; w < W - 1; ++w)
 #pragma unroll
         for (int i = 0; i < 16; ++i) s[i] = s[i] + red[(w * 16 + i) * 64 + lane];
-      if (ks == 1) {
+      if (W == 8 || ks == 1) {  // 8-wave plan: always the whole K (no split-K code at all)
         decode_epilogue<NS, EPI>(s, cs, mt0 + mt, nt, lane, stage, e);
       } else {
         // write-through (sc1) slab stores: visible device-wide once drained,
@@ -489,7 +558,7 @@ __global__ __launch_bounds__(256) void q4_gemm_decode_kernel(const uint8_t* __re
     }
     __syncthreads();
   }
-  if (ks == 1 || wave != 0) return;
+  if (W == 8 || ks == 1 || wave != 0) return;
 
   // split-K fix-up: wave 0 of each slice drained its sc1 stores, one ticket
   // per slice; the slice drawing ks-1 sums all slabs in slice order with sc1
@@ -542,15 +611,32 @@ static size_t prefill_lds_bytes(int ns, int epi) {
   return a > s ? a : s;
 }
 
-static size_t decode_lds_bytes() {
-  return (size_t)(kDecodeWaves - 1) * 16 * 64 * 4 + (size_t)32 * kStageLd * 4;
+static size_t decode_lds_bytes(int w) {
+  return (size_t)(w == 8 ? w : w - 1) * 16 * 64 * 4 + (size_t)32 * kStageLd * 4;
 }
 
 DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal) {
   // Smallest per-wave depth whose grid still covers ~all CUs, then balance.
   static const int pers[3] = {4, 2, 1};
-  DecodePlan p{1, 1, 1};
+  DecodePlan p{1, 1, 1, kDecodeWaves};
   (void)mreal;  // the plan depends on (N, K) only: batch-invariant rows
+  // K <= 1536: one 8-wave workgroup per n-tile holds the whole K range (no
+  // split-K hand-off at all); the grid is N / 32 workgroups.
+  static const bool w8 = [] {
+    const char* env = getenv("WQ4_DECODE_W8");  // tuning knob (tools/q4_bench.py)
+    return env ? atoi(env) != 0 : true;
+  }();
+  if (w8 && nbp <= 8 * kDecodeMaxPer8 * kDecodeMaxKs && ntiles <= kDecodeMaxTiles) {
+    // larger K: the same 8-wave workgroups over ks K slices (sc1 slabs +
+    // last-arriver merge); ks depends on K only
+    p.w = 8;
+    p.ks = (int)((nbp + 8 * kDecodeMaxPer8 - 1) / (8 * kDecodeMaxPer8));
+    while (p.ks > 1 && ntiles * p.ks * 1024 > (int64_t)kDecodeWsFloats) --p.ks;  // workspace bound
+    p.chunk = (int)((nbp + 8 * p.ks - 1) / (8 * p.ks));
+    p.per = p.chunk;
+    if (p.per <= kDecodeMaxPer8) return p;
+    p = DecodePlan{1, 1, 1, kDecodeWaves};  // does not fit: 4-wave plan below
+  }
   const int max_per = kDecodeMaxPer;
   int per = 1;
   for (int c : pers) {
@@ -609,24 +695,33 @@ static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint3
                                 hipStream_t st) {
   const int mtiles = (int)(round_up(rows < 1 ? 1 : rows, kMPad) / kMTile);
   const int mreal0 = (int)((rows + kMTile - 1) / kMTile);
-  if (ws && mreal0 <= kDecodeMaxMTiles && plan_decode(g.ntiles, g.nbp, 2).per <= kDecodeMaxPer) {
-    const DecodePlan p = plan_decode(g.ntiles, g.nbp, 2);
+  const DecodePlan p = plan_decode(g.ntiles, g.nbp, 2);
+  const bool dec_ok = ws && mreal0 <= kDecodeMaxMTiles && p.per <= (p.w == 8 ? kDecodeMaxPer8 : kDecodeMaxPer);
+  if (dec_ok) {
     const dim3 grid((unsigned)(g.ntiles * p.ks));
-#define WQ4_DEC(PER_, MT_)                                                                                   \
-  hipLaunchKernelGGL((q4_gemm_decode_kernel<NS, EPI, PER_, MT_>), grid, dim3(64 * kDecodeWaves),              \
-                     decode_lds_bytes(), st, nib, sc, cs, at, mt0, (int)g.nbp, p.ks, p.chunk, ws->part,           \
-                     ws->counters, e)
-    // m-tiles in launches of <= 2 (each launch completes before the next on
-    // this stream, so they share the workspace and counters)
-    for (int mt0 = 0; mt0 < mreal0; mt0 += 2) {
-      if (mreal0 - mt0 == 1) {
-        if (p.per == 1) WQ4_DEC(1, 1);
-        else if (p.per == 2) WQ4_DEC(2, 1);
-        else WQ4_DEC(4, 1);
-      } else {
-        if (p.per == 1) WQ4_DEC(1, 2);
-        else if (p.per == 2) WQ4_DEC(2, 2);
-        else WQ4_DEC(4, 2);
+#define WQ4_DEC(PER_, MT_, W_)                                                                               \
+  hipLaunchKernelGGL((q4_gemm_decode_kernel<NS, EPI, PER_, MT_, W_>), grid, dim3(64 * W_), decode_lds_bytes(W_), \
+                     st, nib, sc, cs, at, mt0, (int)g.nbp, p.ks, p.chunk, ws->part, ws->counters, e)
+    // 8-wave plans: one m-tile per launch (two would not fit the registers);
+    // 4-wave plans: m-tiles in launches of <= 2.  Launches on one stream
+    // complete in order, so they share the workspace and counters.
+    if (p.w == 8) {
+      for (int mt0 = 0; mt0 < mreal0; ++mt0) {
+        if (p.per == 1) WQ4_DEC(1, 1, 8);
+        else if (p.per == 2) WQ4_DEC(2, 1, 8);
+        else WQ4_DEC(3, 1, 8);
+      }
+    } else {
+      for (int mt0 = 0; mt0 < mreal0; mt0 += 2) {
+        if (mreal0 - mt0 == 1) {
+          if (p.per == 1) WQ4_DEC(1, 1, 4);
+          else if (p.per == 2) WQ4_DEC(2, 1, 4);
+          else WQ4_DEC(4, 1, 4);
+        } else {
+          if (p.per == 1) WQ4_DEC(1, 2, 4);
+          else if (p.per == 2) WQ4_DEC(2, 2, 4);
+          else WQ4_DEC(4, 2, 4);
+        }
       }
     }
 #undef WQ4_DEC
