@@ -154,6 +154,12 @@ wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void
                           float* y_dev, void* at_out_dev, int64_t rows, unsigned flags, wq4_precision prec,
                           int kernel, void* stream);
 
+/* Allocate (once) the per-(device, stream) split-K workspace that small-M
+ * GEMMs on `stream` use.  The first small-M GEMM on a stream does this
+ * itself, which is not allowed inside a graph capture: call this first when
+ * capturing such GEMMs into a hipGraph. */
+wq4_status wq4_prepare_stream(int device, void* stream);
+
 /* LayerNorm (src/model/layers.rs:12-32: eps 1e-5, biased variance) of
  * rows x d f32 rows, written either as the A-tiled operand of a following
  * GEMM with K = d (at_out_dev, wq4_atiled_bytes(rows, d, prec) bytes) or as

@@ -355,8 +355,9 @@ int cross_attention_splits(int T) {
 }
 
 template <int NS, int TQ>
-__global__ __launch_bounds__(256) void cross_attn_kernel(const float* __restrict__ q, const float* __restrict__ kv,
-                                                         int Tq_, int T, int H, int S, float* __restrict__ part,
+__global__ __launch_bounds__(256) void cross_attn_kernel(const float* __restrict__ q, const float* __restrict__ kc,
+                                                         const float* __restrict__ vc, int Tq_, int T, int H, int S,
+                                                         float* __restrict__ part,
                                                          int* __restrict__ counters, _Float16* __restrict__ tiled) {
   // TQ = 1 (decode step) keeps one query's state: ~half the VGPRs, twice the
   // resident waves of the TQ = 4 (prompt) instance
@@ -377,16 +378,17 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const float* __restrict
   const int s0 = split * per_split, s1 = min(T, s0 + per_split);
   const int per_wave = (s1 - s0 + 3) / 4;
   const int k0 = min(s1, s0 + wave * per_wave), k1 = min(s1, k0 + per_wave);
-  // head-major K / V: [2][B][H][T][64] (wq4_gemm_tiled_headmajor)
-  const float* kb = kv + ((size_t)b * H + head) * T * 64 + sub * 4;
-  const size_t vofs = (size_t)gridDim.y * H * T * 64;
+  // head-major K / V: [clip][head][T][64] each (wq4_gemm_tiled_headmajor)
+  const size_t hofs = ((size_t)b * H + head) * T * 64 + sub * 4;
+  const float* kb = kc + hofs;
+  const float* vb = vc + hofs;
   float m[TQ], l[TQ];
   floatx4 o[TQ];
   attn_scan<TQ, 8>(
       qv, Tq, k0, k1, grp,
       [&](int j, const float*& kp, const float*& vp) {
         kp = kb + (size_t)j * 64;
-        vp = kp + vofs;
+        vp = vb + (size_t)j * 64;
       },
       [](int, int) { return true; }, m, l, o);
   float mn, ls, os;
@@ -445,13 +447,13 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const float* __restrict
   }
 }
 
-hipError_t launch_cross_attention(const float* q, const float* kv, int B, int Tq, int T, int H, float* part,
-                                  int* counters, _Float16* tiled, int ns, hipStream_t st) {
+hipError_t launch_cross_attention(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
+                                  float* part, int* counters, _Float16* tiled, int ns, hipStream_t st) {
   if (Tq > 4) return hipErrorInvalidValue;
   const int S = cross_attention_splits(T);
   const dim3 grid(H * S, B), block(256);
 #define WA_XATTN(NS_, TQ_) \
-  hipLaunchKernelGGL((cross_attn_kernel<NS_, TQ_>), grid, block, 0, st, q, kv, Tq, T, H, S, part, counters, tiled)
+  hipLaunchKernelGGL((cross_attn_kernel<NS_, TQ_>), grid, block, 0, st, q, k, v, Tq, T, H, S, part, counters, tiled)
   if (ns == 2) {
     if (Tq == 1) WA_XATTN(2, 1); else WA_XATTN(2, 4);
   } else {

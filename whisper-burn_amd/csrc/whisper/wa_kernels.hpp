@@ -32,12 +32,13 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
 
 // Cross-attention over cached encoder K/V (attention.rs:161-236).  q: [B*Tq,
 // D] f32; kv: [B*T, 2D] f32 (k | v).  Writes the A-tiled operand.
-// Cross-attention over the cached encoder K/V; part / counters: split-merge
+// Cross-attention over the cached encoder K / V (head-major [clip][head][T][64]
+// at k and v); part / counters: split-merge
 // workspace (cross_attention_part_floats floats, B * H zeroed ints).
 int cross_attention_splits(int T);
 size_t cross_attention_part_floats(int B, int H, int T);
-hipError_t launch_cross_attention(const float* q, const float* kv, int B, int Tq, int T, int H, float* part,
-                                  int* counters, _Float16* tiled, int ns, hipStream_t st);
+hipError_t launch_cross_attention(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
+                                  float* part, int* counters, _Float16* tiled, int ns, hipStream_t st);
 
 // Conv1D (layers.rs:77-132) as an implicit-im2col f32 MFMA GEMM + bias +
 // GELU (encoder.rs:89-94) (+ pos[t] if pos != nullptr).  Input element

@@ -146,6 +146,28 @@ struct DecLayer {
   float *cache_k, *cache_v, *cross_kv;
 };
 
+// One decode group: a contiguous range of clips [b0, b0 + nb) decoded on its
+// own stream with its own activations, DecodeState and step graph.  The
+// decode step is a chain of ~350 small dependent kernels (latency-bound);
+// groups on separate streams overlap one another's launch gaps and let the
+// HBM-bound cross-attention of one group run beside the latency-bound GEMMs
+// of another.  Per-clip results do not depend on the grouping (every
+// kernel's per-row arithmetic is independent of the batch).
+constexpr int kMaxGroups = 4;
+struct DecGroup {
+  hipStream_t st = nullptr;
+  int b0 = 0, nb = 0;
+  float *xd, *qkvd, *qd, *hid, *logits;
+  _Float16 *atd_dec, *atf_dec;
+  int *prompt_tok, *next_tok, *tokens, *ntok, *done;
+  float* xattn_part;    // cross-attention split partials
+  int* xattn_counters;  // per (clip, head) arrival tickets, re-armed in-kernel
+  wa::DecodeState* state;
+  int* host_ndone = nullptr;  // pinned ring
+  hipGraphExec_t graph = nullptr;
+  int graph_key = -1;
+};
+
 }  // namespace
 
 struct wa_model {
@@ -161,19 +183,14 @@ struct wa_model {
   float *tok_emb, *dec_pos, *dln_w, *dln_b;
   std::vector<EncLayer> enc;
   std::vector<DecLayer> dec;
-  // activations
-  float *h1, *x, *qkv, *xd, *qkvd, *qd, *hid, *logits;
-  _Float16 *at_d, *at_f, *enc_at, *atd_dec, *atf_dec;
-  int *prompt_tok, *next_tok, *tokens, *ntok, *done;
-  float* xattn_part;     // cross-attention split partials
-  int* xattn_counters;   // per (clip, head) arrival tickets, re-armed in-kernel
-  wa::DecodeState* state;
-  int* host_ndone = nullptr;  // pinned ring
-  // step graph
-  hipGraphExec_t graph = nullptr;
-  int graph_b = -1;
-  hipStream_t graph_stream = nullptr;
-  hipStream_t own_stream = nullptr;  // transcribe runs here (graph capture needs a non-null stream)
+  // encoder activations
+  float *h1, *x, *qkv;
+  _Float16 *at_d, *at_f, *enc_at;
+  // decode groups: the clips of a transcribe split over up to kMaxGroups
+  // independent streams, each replaying its own step graph (see DecGroup)
+  std::vector<DecGroup> groups;
+  int kv_batch = 0;  // clips of the last cross-K/V pass (V half offset of the head-major cache)
+  hipStream_t own_stream = nullptr;  // encoder / cross-K/V (graph capture needs a non-null stream)
   float timings[5] = {0, 0, 0, 0, 0};
   // live kernel timing (wa_profile_*)
   struct Pending {
@@ -202,9 +219,12 @@ struct wa_model {
 
   ~wa_model() {
     resolve_profile();
-    if (graph) (void)hipGraphExecDestroy(graph);
+    for (auto& g : groups) {
+      if (g.graph) (void)hipGraphExecDestroy(g.graph);
+      if (g.st) (void)hipStreamDestroy(g.st);
+      if (g.host_ndone) (void)hipHostFree(g.host_ndone);
+    }
     if (own_stream) (void)hipStreamDestroy(own_stream);
-    if (host_ndone) (void)hipHostFree(host_ndone);
     for (auto& l : enc)
       for (wq4_tensor* t : {l.qkv, l.out, l.fc1, l.fc2}) wq4_tensor_destroy(t);
     for (auto& l : dec)
@@ -367,27 +387,34 @@ wq4_status alloc_activations(wa_model* m) {
     L.cache_v = f32((int64_t)B * c.n_text_ctx * Dt);
     L.cross_kv = f32(renc * 2 * Dt);
   }
-  m->xd = f32(rdec * Dt);
-  m->qkvd = f32(rdec * 3 * Dt);
-  m->qd = f32(rdec * Dt);
-  m->hid = f32(rdec * Dt);
-  m->logits = f32((int64_t)B * c.n_vocab);
-  m->atd_dec = tiled(rdec, Dt);
-  m->atf_dec = tiled(rdec, Ft);
-  m->prompt_tok = d.alloc<int>(rdec);
-  m->next_tok = d.alloc<int>(B);
-  m->tokens = d.alloc<int>((size_t)B * kMaxTokens);
-  m->ntok = d.alloc<int>(B);
-  m->done = d.alloc<int>(B);
-  m->state = d.alloc<wa::DecodeState>(1);
-  m->xattn_part = f32((int64_t)wa::cross_attention_part_floats(B, c.n_text_head, T));
-  m->xattn_counters = d.alloc<int>((size_t)B * c.n_text_head);
-  if (!m->xattn_part || !m->xattn_counters) return fail(WQ4_ENOMEM, "cross-attention workspace allocation failed");
-  WA_HIP(hipMemset(m->xattn_counters, 0, (size_t)B * c.n_text_head * sizeof(int)));
-  for (void* p : {(void*)m->h1, (void*)m->x, (void*)m->qkv, (void*)m->at_d, (void*)m->at_f, (void*)m->enc_at,
-                  (void*)m->xd, (void*)m->qkvd, (void*)m->qd, (void*)m->hid, (void*)m->logits, (void*)m->atd_dec,
-                  (void*)m->atf_dec, (void*)m->prompt_tok, (void*)m->next_tok, (void*)m->tokens, (void*)m->ntok,
-                  (void*)m->done, (void*)m->state})
+  m->groups.resize(kMaxGroups);
+  for (DecGroup& g : m->groups) {  // each group sized for the whole batch (small)
+    g.xd = f32(rdec * Dt);
+    g.qkvd = f32(rdec * 3 * Dt);
+    g.qd = f32(rdec * Dt);
+    g.hid = f32(rdec * Dt);
+    g.logits = f32((int64_t)B * c.n_vocab);
+    g.atd_dec = tiled(rdec, Dt);
+    g.atf_dec = tiled(rdec, Ft);
+    g.prompt_tok = d.alloc<int>(rdec);
+    g.next_tok = d.alloc<int>(B);
+    g.tokens = d.alloc<int>((size_t)B * kMaxTokens);
+    g.ntok = d.alloc<int>(B);
+    g.done = d.alloc<int>(B);
+    g.state = d.alloc<wa::DecodeState>(1);
+    g.xattn_part = f32((int64_t)wa::cross_attention_part_floats(B, c.n_text_head, T));
+    g.xattn_counters = d.alloc<int>((size_t)B * c.n_text_head);
+    for (void* p : {(void*)g.xd, (void*)g.qkvd, (void*)g.qd, (void*)g.hid, (void*)g.logits, (void*)g.atd_dec,
+                    (void*)g.atf_dec, (void*)g.prompt_tok, (void*)g.next_tok, (void*)g.tokens, (void*)g.ntok,
+                    (void*)g.done, (void*)g.state, (void*)g.xattn_part, (void*)g.xattn_counters})
+      if (!p) return fail(WQ4_ENOMEM, "decode-group allocation failed");
+    WA_HIP(hipMemset(g.xattn_counters, 0, (size_t)B * c.n_text_head * sizeof(int)));
+    WA_HIP(hipMemset(g.atd_dec, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
+    WA_HIP(hipMemset(g.atf_dec, 0, wq4_atiled_bytes(rdec, Ft, m->prec)));
+    WA_HIP(hipHostMalloc(reinterpret_cast<void**>(&g.host_ndone), 8 * sizeof(int), 0));
+    WA_HIP(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
+  }
+  for (void* p : {(void*)m->h1, (void*)m->x, (void*)m->qkv, (void*)m->at_d, (void*)m->at_f, (void*)m->enc_at})
     if (!p) return fail(WQ4_ENOMEM, "activation allocation failed");
   for (auto& L : m->dec)
     if (!L.cache_k || !L.cache_v || !L.cross_kv) return fail(WQ4_ENOMEM, "KV cache allocation failed");
@@ -395,9 +422,6 @@ wq4_status alloc_activations(wa_model* m) {
   WA_HIP(hipMemset(m->at_d, 0, wq4_atiled_bytes(renc, D, m->prec)));
   WA_HIP(hipMemset(m->at_f, 0, wq4_atiled_bytes(renc, F, m->prec)));
   WA_HIP(hipMemset(m->enc_at, 0, wq4_atiled_bytes(renc, D, m->prec)));
-  WA_HIP(hipMemset(m->atd_dec, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
-  WA_HIP(hipMemset(m->atf_dec, 0, wq4_atiled_bytes(rdec, Ft, m->prec)));
-  WA_HIP(hipHostMalloc(reinterpret_cast<void**>(&m->host_ndone), 8 * sizeof(int), 0));
   return WQ4_OK;
 }
 
@@ -491,6 +515,7 @@ wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st,
 // (attention.rs:177-206 forward_init_cache, run once per clip).
 wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st) {
   const int64_t rows = (int64_t)B * m->cfg.n_audio_ctx;
+  m->kv_batch = B;
   for (auto& L : m->dec) {
     Prof p = q4prof(m, st, L.ckv, rows);
     // K|V written head-major [2][B][H][T][64]: each (clip, head) streams two
@@ -501,46 +526,137 @@ wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st) {
   return WQ4_OK;
 }
 
-// Decoder pass over Tq new tokens per clip (forward_prompt when state ==
-// nullptr, decode_step otherwise), ending in last-position logits.
-wq4_status decoder_forward(wa_model* m, const int* tokens, int B, int Tq, const wa::DecodeState* state, int pos0,
-                           int kv0, hipStream_t st) {
+// Decoder pass over Tq new tokens for the clips of group g (forward_prompt
+// when state == nullptr, decode_step otherwise), ending in last-position
+// logits.  Self-KV and cross-K/V are addressed at the group's clip offset.
+wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, const wa::DecodeState* state,
+                           int pos0, int kv0, hipStream_t st) {
   const Config& c = m->cfg;
-  const int D = c.n_text_state, H = c.n_text_head;
+  const int D = c.n_text_state, H = c.n_text_head, T = c.n_audio_ctx;
+  const int B = g.nb;
   const int64_t rows = (int64_t)B * Tq;
-  WA_HIP(wa::launch_embed(tokens, m->tok_emb, m->dec_pos, B, Tq, D, state, pos0, m->xd, st));
+  const size_t self_ofs = (size_t)g.b0 * H * c.n_text_ctx * 64;
+  const size_t cross_ofs = (size_t)g.b0 * H * T * 64, cross_v = (size_t)m->kv_batch * H * T * 64;
+  WA_HIP(wa::launch_embed(tokens, m->tok_emb, m->dec_pos, B, Tq, D, state, pos0, g.xd, st));
   for (auto& L : m->dec) {  // DecoderBlock (decoder.rs:77-112 / 140-183)
-    WA_WQ4(wq4_layernorm(m->xd, L.ln1_w, L.ln1_b, rows, D, m->prec, m->atd_dec, nullptr, st));
-    WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, m->atd_dec, nullptr, m->qkvd, nullptr, rows, 0u, m->prec, 2, st));
-    WA_HIP(wa::launch_decoder_self_attention(m->qkvd, L.cache_k, L.cache_v, B, Tq, H, c.n_text_ctx, state, kv0,
-                                             m->atd_dec, m->ns, st));
-    WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, m->atd_dec, m->xd, m->xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
-    WA_WQ4(wq4_layernorm(m->xd, L.ln2_w, L.ln2_b, rows, D, m->prec, m->atd_dec, nullptr, st));
-    WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, m->atd_dec, nullptr, m->qd, nullptr, rows, 0u, m->prec, 2, st));
-    WA_HIP(wa::launch_cross_attention(m->qd, L.cross_kv, B, Tq, c.n_audio_ctx, H, m->xattn_part, m->xattn_counters,
-                                      m->atd_dec, m->ns, st));
-    WA_WQ4(wq4_gemm_tiled(L.cout, L.cout_b, m->atd_dec, m->xd, m->xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2,
-                          st));
-    WA_WQ4(wq4_layernorm(m->xd, L.ln3_w, L.ln3_b, rows, D, m->prec, m->atd_dec, nullptr, st));
-    WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, m->atd_dec, nullptr, nullptr, m->atf_dec, rows,
+    WA_WQ4(wq4_layernorm(g.xd, L.ln1_w, L.ln1_b, rows, D, m->prec, g.atd_dec, nullptr, st));
+    WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, g.atd_dec, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, 2, st));
+    WA_HIP(wa::launch_decoder_self_attention(g.qkvd, L.cache_k + self_ofs, L.cache_v + self_ofs, B, Tq, H,
+                                             c.n_text_ctx, state, kv0, g.atd_dec, m->ns, st));
+    WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
+    WA_WQ4(wq4_layernorm(g.xd, L.ln2_w, L.ln2_b, rows, D, m->prec, g.atd_dec, nullptr, st));
+    WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, g.atd_dec, nullptr, g.qd, nullptr, rows, 0u, m->prec, 2, st));
+    WA_HIP(wa::launch_cross_attention(g.qd, L.cross_kv + cross_ofs, L.cross_kv + cross_v + cross_ofs, B, Tq, T, H,
+                                      g.xattn_part, g.xattn_counters, g.atd_dec, m->ns, st));
+    WA_WQ4(wq4_gemm_tiled(L.cout, L.cout_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
+    WA_WQ4(wq4_layernorm(g.xd, L.ln3_w, L.ln3_b, rows, D, m->prec, g.atd_dec, nullptr, st));
+    WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, g.atd_dec, nullptr, nullptr, g.atf_dec, rows,
                           WQ4_EPI_GELU | WQ4_EPI_TILED_OUT, m->prec, 2, st));
-    WA_WQ4(wq4_gemm_tiled(L.fc2, L.fc2_b, m->atf_dec, m->xd, m->xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
+    WA_WQ4(wq4_gemm_tiled(L.fc2, L.fc2_b, g.atf_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
   }
   // final LN (decoder.rs:286 / 340) and tied-embedding logits of the last
   // position of every clip (decoder.rs:289-292, 342-343)
-  WA_WQ4(wq4_layernorm(m->xd, m->dln_w, m->dln_b, rows, D, WQ4_PREC_F16X2, nullptr, m->hid, st));
-  WA_HIP(wa::launch_logits(m->hid + (size_t)(Tq - 1) * D, B, D, (int64_t)Tq * D, m->tok_emb, c.n_vocab, m->logits,
+  WA_WQ4(wq4_layernorm(g.xd, m->dln_w, m->dln_b, rows, D, WQ4_PREC_F16X2, nullptr, g.hid, st));
+  WA_HIP(wa::launch_logits(g.hid + (size_t)(Tq - 1) * D, B, D, (int64_t)Tq * D, m->tok_emb, c.n_vocab, g.logits,
                            st));
   return WQ4_OK;
 }
 
 // One greedy step (whisper.rs:104-125): bookkeeping, decode_step, argmax.
-wq4_status decode_step(wa_model* m, int B, int eot_stop, hipStream_t st) {
-  WA_HIP(wa::launch_bookkeep(m->next_tok, m->tokens, m->ntok, m->done, B, kMaxTokens, eot_stop, m->state, st));
-  wq4_status s = decoder_forward(m, m->next_tok, B, 1, m->state, 0, 0, st);
+wq4_status decode_step(wa_model* m, DecGroup& g, int eot_stop, hipStream_t st) {
+  WA_HIP(wa::launch_bookkeep(g.next_tok, g.tokens, g.ntok, g.done, g.nb, kMaxTokens, eot_stop, g.state, st));
+  wq4_status s = decoder_forward(m, g, g.next_tok, 1, g.state, 0, 0, st);
   if (s != WQ4_OK) return s;
-  WA_HIP(wa::launch_argmax_step(m->logits, B, m->cfg.n_vocab, kMinTokens, m->state, m->next_tok, st));
+  WA_HIP(wa::launch_argmax_step(g.logits, g.nb, m->cfg.n_vocab, kMinTokens, g.state, g.next_tok, st));
   return WQ4_OK;
+}
+
+// Prompt of group g (whisper.rs:60-99), leaving the first greedy token in
+// next_tok and the DecodeState ready for the step graph.
+wq4_status prompt_group(wa_model* m, DecGroup& g, int lang_token, hipStream_t st) {
+  const Config& c = m->cfg;
+  const int B = g.nb;
+  std::vector<int> ptok((size_t)B * 4);
+  int pos0, kv0;
+  wq4_status s;
+  if (lang_token >= 0) {
+    for (int b = 0; b < B; ++b) {
+      ptok[b * 4 + 0] = kSOT;
+      ptok[b * 4 + 1] = lang_token;
+      ptok[b * 4 + 2] = c.transcribe_token();
+      ptok[b * 4 + 3] = c.no_timestamps_token();
+    }
+    WA_HIP(hipMemcpyAsync(g.prompt_tok, ptok.data(), (size_t)B * 4 * 4, hipMemcpyHostToDevice, st));
+    s = decoder_forward(m, g, g.prompt_tok, 4, nullptr, 0, 0, st);
+    if (s != WQ4_OK) return s;
+    pos0 = 4;
+    kv0 = 4;
+  } else {
+    // decode_step(SOT, 0) fills a 1-entry cache; the language is the last max
+    // over the language-token range (whisper.rs:73-83) ...
+    for (int b = 0; b < B; ++b) {
+      ptok[b * 3 + 0] = kSOT;
+      ptok[b * 3 + 1] = c.transcribe_token();
+      ptok[b * 3 + 2] = c.no_timestamps_token();
+    }
+    WA_HIP(hipMemcpyAsync(g.prompt_tok, ptok.data(), (size_t)B * 3 * 4, hipMemcpyHostToDevice, st));
+    // SOT rows: embed reads tokens[b * Tq + t] with Tq = 1 -> a contiguous [B]
+    // array: next_tok as scratch
+    std::vector<int> sot(B, kSOT);
+    WA_HIP(hipMemcpyAsync(g.next_tok, sot.data(), (size_t)B * 4, hipMemcpyHostToDevice, st));
+    s = decoder_forward(m, g, g.next_tok, 1, nullptr, 0, 0, st);
+    if (s != WQ4_OK) return s;
+    WA_HIP(wa::launch_argmax(g.logits, B, c.n_vocab, 50259, 50259 + c.n_lang, 0, nullptr, g.prompt_tok, 3, st));
+    // ... then forward_prompt([lang, TRANSCRIBE, NO_TIMESTAMPS]) OVERWRITES the
+    // cache from index 0 with positions 0..2 (decoder.rs:272-283) while the
+    // position counter continues at 1 + 3 = 4 (whisper.rs:74,93).
+    s = decoder_forward(m, g, g.prompt_tok, 3, nullptr, 0, 0, st);
+    if (s != WQ4_OK) return s;
+    pos0 = 4;
+    kv0 = 3;
+  }
+  // first token: EOT suppressed (whisper.rs:97-99)
+  WA_HIP(wa::launch_argmax(g.logits, B, c.n_vocab, 0, c.n_vocab, 1, nullptr, g.next_tok, 1, st));
+  const wa::DecodeState init{pos0 - 1, kv0 - 1, -1, 0};
+  WA_HIP(hipMemcpyAsync(g.state, &init, sizeof(init), hipMemcpyHostToDevice, st));
+  WA_HIP(hipMemsetAsync(g.ntok, 0, (size_t)B * 4, st));
+  WA_HIP(hipMemsetAsync(g.done, 0, (size_t)B * 4, st));
+  WA_HIP(hipMemsetAsync(g.tokens, 0, (size_t)B * kMaxTokens * 4, st));
+  return WQ4_OK;
+}
+
+// Capture (once per group size / eot mode) the step graph of group g.
+wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
+  const int key = g.nb * 2 + (eot_stop ? 1 : 0);
+  if (g.graph && g.graph_key == key) return WQ4_OK;
+  if (g.graph) {
+    (void)hipGraphExecDestroy(g.graph);
+    g.graph = nullptr;
+  }
+  WA_WQ4(wq4_prepare_stream(m->device, g.st));  // split-K workspace exists before capture
+  hipGraph_t gr;
+  WA_HIP(hipStreamBeginCapture(g.st, hipStreamCaptureModeThreadLocal));
+  wq4_status s = decode_step(m, g, eot_stop, g.st);
+  hipError_t ce = hipStreamEndCapture(g.st, &gr);
+  if (s != WQ4_OK) return s;
+  if (ce != hipSuccess) return fail(WQ4_EHIP, std::string("graph capture: ") + hipGetErrorString(ce));
+  ce = hipGraphInstantiate(&g.graph, gr, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(gr);
+  if (ce != hipSuccess) return fail(WQ4_EHIP, std::string("graph instantiate: ") + hipGetErrorString(ce));
+  g.graph_key = key;
+  return WQ4_OK;
+}
+
+// Number of decode groups for a batch (WA_DECODE_GROUPS overrides).
+int decode_groups(int B) {
+  static const int forced = [] {
+    const char* env = getenv("WA_DECODE_GROUPS");
+    return env ? atoi(env) : 0;
+  }();
+  int G = forced > 0 ? forced : (B >= 16 ? 2 : 1);
+  if (G > kMaxGroups) G = kMaxGroups;
+  if (G > B) G = B;
+  return G;
 }
 
 }  // namespace
@@ -628,11 +744,15 @@ wq4_status wa_prompt_logits(wa_model* m, const int32_t* prompt_dev, int n_clips,
                             void* stream) {
   if (!m || !prompt_dev || !logits_dev) return fail(WQ4_EINVAL, "null argument");
   if (n_clips < 1 || n_clips > m->bmax || plen < 1 || plen > 4) return fail(WQ4_EINVAL, "bad n_clips / plen");
+  if (n_clips > m->kv_batch) return fail(WQ4_EINVAL, "wa_encode the clips first");
   WA_HIP(hipSetDevice(m->device));
   hipStream_t st = static_cast<hipStream_t>(stream);
-  wq4_status s = decoder_forward(m, prompt_dev, n_clips, plen, nullptr, 0, 0, st);
+  DecGroup& g = m->groups[0];
+  g.b0 = 0;
+  g.nb = n_clips;
+  wq4_status s = decoder_forward(m, g, prompt_dev, plen, nullptr, 0, 0, st);
   if (s != WQ4_OK) return s;
-  WA_HIP(hipMemcpyAsync(logits_dev, m->logits, (size_t)n_clips * m->cfg.n_vocab * 4, hipMemcpyDeviceToDevice, st));
+  WA_HIP(hipMemcpyAsync(logits_dev, g.logits, (size_t)n_clips * m->cfg.n_vocab * 4, hipMemcpyDeviceToDevice, st));
   return WQ4_OK;
 }
 
@@ -644,7 +764,6 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
   WA_HIP(hipSetDevice(m->device));
   // all work on the model's own stream, ordered after the caller's stream
   hipStream_t st = m->own_stream;
-  const Config& c = m->cfg;
   const int B = n_clips;
   hipEvent_t ev[5];
   for (auto& e : ev) WA_HIP(hipEventCreate(&e));
@@ -665,114 +784,115 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
   if (s != WQ4_OK) return s;
   WA_HIP(hipEventRecord(ev[2], st));
 
-  // prompt (whisper.rs:60-99)
-  std::vector<int> ptok((size_t)B * 4);
-  int pos0, kv0;
-  if (lang_token >= 0) {
-    for (int b = 0; b < B; ++b) {
-      ptok[b * 4 + 0] = kSOT;
-      ptok[b * 4 + 1] = lang_token;
-      ptok[b * 4 + 2] = c.transcribe_token();
-      ptok[b * 4 + 3] = c.no_timestamps_token();
-    }
-    WA_HIP(hipMemcpyAsync(m->prompt_tok, ptok.data(), (size_t)B * 4 * 4, hipMemcpyHostToDevice, st));
-    s = decoder_forward(m, m->prompt_tok, B, 4, nullptr, 0, 0, st);
-    if (s != WQ4_OK) return s;
-    pos0 = 4;
-    kv0 = 4;
-  } else {
-    // decode_step(SOT, 0) fills a 1-entry cache; the language is the last max
-    // over the language-token range (whisper.rs:73-83) ...
-    for (int b = 0; b < B; ++b) {
-      ptok[b * 3 + 0] = kSOT;
-      ptok[b * 3 + 1] = c.transcribe_token();
-      ptok[b * 3 + 2] = c.no_timestamps_token();
-    }
-    WA_HIP(hipMemcpyAsync(m->prompt_tok, ptok.data(), (size_t)B * 3 * 4, hipMemcpyHostToDevice, st));
-    // SOT rows: prompt_tok[b*3] (embed reads tokens[b*Tq + t] with Tq = 1 ->
-    // needs a contiguous [B] array: use next_tok as scratch)
-    std::vector<int> sot(B, kSOT);
-    WA_HIP(hipMemcpyAsync(m->next_tok, sot.data(), (size_t)B * 4, hipMemcpyHostToDevice, st));
-    s = decoder_forward(m, m->next_tok, B, 1, nullptr, 0, 0, st);
-    if (s != WQ4_OK) return s;
-    WA_HIP(wa::launch_argmax(m->logits, B, c.n_vocab, 50259, 50259 + c.n_lang, 0, nullptr, m->prompt_tok, 3, st));
-    // ... then forward_prompt([lang, TRANSCRIBE, NO_TIMESTAMPS]) OVERWRITES the
-    // cache from index 0 with positions 0..2 (decoder.rs:272-283) while the
-    // position counter continues at 1 + 3 = 4 (whisper.rs:74,93).
-    s = decoder_forward(m, m->prompt_tok, B, 3, nullptr, 0, 0, st);
-    if (s != WQ4_OK) return s;
-    pos0 = 4;
-    kv0 = 3;
+  // decode groups: contiguous clip ranges on their own streams, started
+  // after the cross-K/V pass, joined back into `st` at the end
+  const int G = decode_groups(B);
+  hipEvent_t kv_ready, gdone[kMaxGroups], gprompt[kMaxGroups];
+  WA_HIP(hipEventCreateWithFlags(&kv_ready, hipEventDisableTiming));
+  for (int i = 0; i < G; ++i) {
+    WA_HIP(hipEventCreate(&gdone[i]));
+    WA_HIP(hipEventCreate(&gprompt[i]));
   }
-  // first token: EOT suppressed (whisper.rs:97-99)
-  WA_HIP(wa::launch_argmax(m->logits, B, c.n_vocab, 0, c.n_vocab, 1, nullptr, m->next_tok, 1, st));
-  const wa::DecodeState init{pos0 - 1, kv0 - 1, -1, 0};
-  WA_HIP(hipMemcpyAsync(m->state, &init, sizeof(init), hipMemcpyHostToDevice, st));
-  WA_HIP(hipMemsetAsync(m->ntok, 0, (size_t)B * 4, st));
-  WA_HIP(hipMemsetAsync(m->done, 0, (size_t)B * 4, st));
-  WA_HIP(hipMemsetAsync(m->tokens, 0, (size_t)B * kMaxTokens * 4, st));
-  WA_HIP(hipEventRecord(ev[3], st));
-
-  // greedy loop (whisper.rs:104-125), one replayed graph per step
-  if (!m->graph || m->graph_b != B * 2 + (eot_stop ? 1 : 0) || m->graph_stream != st) {
-    if (m->graph) {
-      (void)hipGraphExecDestroy(m->graph);
-      m->graph = nullptr;
+  struct GEvGuard {
+    hipEvent_t* k;
+    hipEvent_t* d;
+    hipEvent_t* p;
+    int n;
+    ~GEvGuard() {
+      (void)hipEventDestroy(*k);
+      for (int i = 0; i < n; ++i) {
+        (void)hipEventDestroy(d[i]);
+        (void)hipEventDestroy(p[i]);
+      }
     }
-    hipGraph_t g;
-    WA_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-    s = decode_step(m, B, eot_stop, st);
-    hipError_t ce = hipStreamEndCapture(st, &g);
+  } geg{&kv_ready, gdone, gprompt, G};
+  WA_HIP(hipEventRecord(kv_ready, st));
+  for (int i = 0; i < G; ++i) {
+    DecGroup& g = m->groups[i];
+    g.b0 = (int)((int64_t)B * i / G);
+    g.nb = (int)((int64_t)B * (i + 1) / G) - g.b0;
+    WA_HIP(hipStreamWaitEvent(g.st, kv_ready, 0));
+    s = prompt_group(m, g, lang_token, g.st);
     if (s != WQ4_OK) return s;
-    if (ce != hipSuccess) return fail(WQ4_EHIP, std::string("graph capture: ") + hipGetErrorString(ce));
-    ce = hipGraphInstantiate(&m->graph, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    if (ce != hipSuccess) return fail(WQ4_EHIP, std::string("graph instantiate: ") + hipGetErrorString(ce));
-    m->graph_b = B * 2 + (eot_stop ? 1 : 0);
-    m->graph_stream = st;
+    WA_HIP(hipEventRecord(gprompt[i], g.st));
+    s = ensure_graph(m, g, eot_stop);
+    if (s != WQ4_OK) return s;
   }
-  hipEvent_t ring[8];
-  for (auto& e : ring) WA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  // greedy loop (whisper.rs:104-125): each step replays every live group's
+  // graph; a group stops once all its clips emitted EOT (polled with a lag)
+  hipEvent_t ring[kMaxGroups][8];
+  for (int i = 0; i < G; ++i)
+    for (auto& e : ring[i]) WA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   struct RingGuard {
-    hipEvent_t* e;
+    hipEvent_t (*e)[8];
+    int n;
     ~RingGuard() {
-      for (int i = 0; i < 8; ++i) (void)hipEventDestroy(e[i]);
+      for (int i = 0; i < n; ++i)
+        for (int j = 0; j < 8; ++j) (void)hipEventDestroy(e[i][j]);
     }
-  } rg{ring};
+  } rg{ring, G};
   int steps = 0;
   const int lag = 4;
-  for (int step = 0; step < max_tokens; ++step) {
-    WA_HIP(hipGraphLaunch(m->graph, st));
+  bool live[kMaxGroups] = {};
+  int nlive = G;
+  for (int i = 0; i < G; ++i) live[i] = true;
+  for (int step = 0; step < max_tokens && nlive > 0; ++step) {
+    for (int i = 0; i < G; ++i) {
+      if (!live[i]) continue;
+      DecGroup& g = m->groups[i];
+      WA_HIP(hipGraphLaunch(g.graph, g.st));
+      if (eot_stop) {
+        const int slot = step % 8;
+        WA_HIP(hipMemcpyAsync(&g.host_ndone[slot], &g.state->n_done, sizeof(int), hipMemcpyDeviceToHost, g.st));
+        WA_HIP(hipEventRecord(ring[i][slot], g.st));
+      }
+    }
     ++steps;
-    if (eot_stop) {
-      const int slot = step % 8;
-      WA_HIP(hipMemcpyAsync(&m->host_ndone[slot], &m->state->n_done, sizeof(int), hipMemcpyDeviceToHost, st));
-      WA_HIP(hipEventRecord(ring[slot], st));
-      if (step >= lag) {
-        const int old = (step - lag) % 8;
-        WA_HIP(hipEventSynchronize(ring[old]));
-        if (m->host_ndone[old] >= B) break;  // every clip had emitted EOT by then
+    if (eot_stop && step >= lag) {
+      const int old = (step - lag) % 8;
+      for (int i = 0; i < G; ++i) {
+        if (!live[i]) continue;
+        WA_HIP(hipEventSynchronize(ring[i][old]));
+        if (m->groups[i].host_ndone[old] >= m->groups[i].nb) {  // every clip had emitted EOT by then
+          live[i] = false;
+          --nlive;
+        }
       }
     }
   }
   // the loop's bookkeeping for tokens chosen by the last step happens at the
   // top of a step that the reference never runs: nothing to add.
+  for (int i = 0; i < G; ++i) {
+    WA_HIP(hipEventRecord(gdone[i], m->groups[i].st));
+    WA_HIP(hipStreamWaitEvent(st, gdone[i], 0));
+  }
   WA_HIP(hipEventRecord(ev[4], st));
   std::vector<int32_t> tok((size_t)B * kMaxTokens), nt(B);
-  WA_HIP(hipMemcpyAsync(tok.data(), m->tokens, tok.size() * 4, hipMemcpyDeviceToHost, st));
-  WA_HIP(hipMemcpyAsync(nt.data(), m->ntok, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+  for (int i = 0; i < G; ++i) {
+    const DecGroup& g = m->groups[i];
+    WA_HIP(hipMemcpyAsync(tok.data() + (size_t)g.b0 * kMaxTokens, g.tokens, (size_t)g.nb * kMaxTokens * 4,
+                          hipMemcpyDeviceToHost, st));
+    WA_HIP(hipMemcpyAsync(nt.data() + g.b0, g.ntok, (size_t)g.nb * 4, hipMemcpyDeviceToHost, st));
+  }
   WA_HIP(hipStreamSynchronize(st));
   for (int b = 0; b < B; ++b) {
     n_tokens_out[b] = std::min(nt[b], max_tokens);
     std::memcpy(tokens_out + (size_t)b * max_tokens, tok.data() + (size_t)b * kMaxTokens,
                 (size_t)max_tokens * 4);
   }
-  float ms[4];
-  for (int i = 0; i < 4; ++i) WA_HIP(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
+  // phases: encoder, cross-K/V, prompt (slowest group), decode loop
+  float ms[3], tp = 0.0f, tall = 0.0f;
+  for (int i = 0; i < 2; ++i) WA_HIP(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
+  for (int i = 0; i < G; ++i) {
+    float t = 0.0f;
+    WA_HIP(hipEventElapsedTime(&t, ev[2], gprompt[i]));
+    tp = std::max(tp, t);
+  }
+  WA_HIP(hipEventElapsedTime(&tall, ev[2], ev[4]));
   m->timings[0] = ms[0];
   m->timings[1] = ms[1];
-  m->timings[2] = ms[2];
-  m->timings[3] = ms[3];
+  m->timings[2] = tp;
+  m->timings[3] = tall - tp;
   m->timings[4] = (float)steps;
   return WQ4_OK;
 }
@@ -780,34 +900,37 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
 wq4_status wa_probe_kernels(wa_model* m, int n_clips, int iters, double* out) {
   if (!m || !out) return fail(WQ4_EINVAL, "null argument");
   if (n_clips < 1 || n_clips > m->bmax || iters < 1) return fail(WQ4_EINVAL, "bad n_clips / iters");
+  if (n_clips > m->kv_batch) return fail(WQ4_EINVAL, "run wa_transcribe / wa_encode on n_clips clips first");
   WA_HIP(hipSetDevice(m->device));
   hipStream_t st = m->own_stream;
   const Config& c = m->cfg;
-  const int B = n_clips, D = c.n_text_state, T = c.n_audio_ctx;
+  const int B = n_clips, D = c.n_text_state, T = c.n_audio_ctx, H = c.n_text_head;
   DecLayer& L = m->dec[0];
+  DecGroup& g = m->groups[0];
+  const float* kb = L.cross_kv;
+  const float* vb = L.cross_kv + (size_t)m->kv_batch * H * T * 64;
   hipEvent_t a, b;
   WA_HIP(hipEventCreate(&a));
   WA_HIP(hipEventCreate(&b));
   float ms = 0.0f;
   // cross-attention of one decode step (Tq = 1): reads K and V of every clip
-  WA_HIP(wa::launch_cross_attention(m->qd, L.cross_kv, B, 1, T, c.n_text_head, m->xattn_part, m->xattn_counters,
-                                    m->atd_dec, m->ns, st));
+  WA_HIP(wa::launch_cross_attention(g.qd, kb, vb, B, 1, T, H, g.xattn_part, g.xattn_counters, g.atd_dec, m->ns, st));
   WA_HIP(hipEventRecord(a, st));
   for (int i = 0; i < iters; ++i)
-    WA_HIP(wa::launch_cross_attention(m->qd, L.cross_kv, B, 1, T, c.n_text_head, m->xattn_part, m->xattn_counters,
-                                      m->atd_dec, m->ns, st));
+    WA_HIP(wa::launch_cross_attention(g.qd, kb, vb, B, 1, T, H, g.xattn_part, g.xattn_counters, g.atd_dec, m->ns,
+                                      st));
   WA_HIP(hipEventRecord(b, st));
   WA_HIP(hipEventSynchronize(b));
   WA_HIP(hipEventElapsedTime(&ms, a, b));
   out[0] = ms * 1e3 / iters;
   out[1] = (double)B * T * 2 * D * 4 + (double)B * D * (4 + 2 * m->ns);
-  // fc1 of one decode step (M = n_clips rows, split-K decode kernel, tiled out)
+  // fc1 of one decode step (M = n_clips rows, decode kernel, GELU + tiled out)
   const int F = 4 * D;
-  WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, m->atd_dec, nullptr, nullptr, m->atf_dec, B, WQ4_EPI_GELU | WQ4_EPI_TILED_OUT,
+  WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, g.atd_dec, nullptr, nullptr, g.atf_dec, B, WQ4_EPI_GELU | WQ4_EPI_TILED_OUT,
                         m->prec, 2, st));
   WA_HIP(hipEventRecord(a, st));
   for (int i = 0; i < iters; ++i)
-    WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, m->atd_dec, nullptr, nullptr, m->atf_dec, B,
+    WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, g.atd_dec, nullptr, nullptr, g.atf_dec, B,
                           WQ4_EPI_GELU | WQ4_EPI_TILED_OUT, m->prec, 2, st));
   WA_HIP(hipEventRecord(b, st));
   WA_HIP(hipEventSynchronize(b));

@@ -541,6 +541,14 @@ wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void
               ns_of(prec), static_cast<hipStream_t>(stream), dec);
 }
 
+wq4_status wq4_prepare_stream(int device, void* stream) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return fail(WQ4_EINVAL, "bad device");
+  DeviceGuard dg(device);
+  const wq4::DecodeWs* ws = nullptr;
+  return decode_ws_get(device, stream, &ws);
+}
+
 wq4_status wq4_layernorm(const float* x_dev, const float* w_dev, const float* b_dev, int64_t rows, int64_t d,
                          wq4_precision prec, void* at_out_dev, float* y_dev, void* stream) {
   wq4_status s = check_prec(prec);
