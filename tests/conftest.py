@@ -14,7 +14,7 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "whisper-burn_amd")
-for p in (REPO, PKG, os.path.join(REPO, "oracle")):
+for p in (REPO, PKG, os.path.join(PKG, "tools"), os.path.join(REPO, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -97,3 +97,44 @@ def test_rejects_bad_arguments(torch, gpu_model):
         gpu_model.transcribe(mel, 50259, max_tokens=225)
     with pytest.raises(wq4.WQ4Error):
         gpu_model.transcribe(torch.from_numpy(mels(5)).cuda(), 50259, max_tokens=4)
+
+
+# ------------------------------------------------- GGUF loader (§8(f) rank 2) --
+def test_gguf_model_equals_synthetic(torch, gpu_model, tmp_path):
+    """load_whisper_from_gguf on a checkpoint written by tools/write_gguf.py
+    (the converter's format) gives the synthetic model bit for bit."""
+    import whisper_amd
+    import write_gguf
+
+    p = tmp_path / "tiny.gguf"
+    write_gguf.write_synthetic_gguf(str(p), "tiny_test", SEED)
+    g = whisper_amd.WhisperModel.from_gguf(str(p), "tiny_test", max_batch=4)
+    mel = torch.from_numpy(mels(2, first=7)).cuda()
+    assert torch.equal(g.encode(mel), gpu_model.encode(mel))
+    assert g.transcribe(mel, 50259, max_tokens=24) == gpu_model.transcribe(mel, 50259, max_tokens=24)
+    g.close()
+
+
+def test_gguf_loader_errors(torch, tmp_path, monkeypatch):
+    import whisper_amd
+    import write_gguf
+
+    tensors = write_gguf.synthetic_tensors("tiny_test", SEED)
+    p = tmp_path / "t.gguf"
+    write_gguf.write_gguf(str(p), tensors, "t")
+    with pytest.raises(wq4.WQ4Error, match="elements, expected|wrong shape"):
+        whisper_amd.WhisperModel.from_gguf(str(p), "medium", max_batch=1)  # D = 1024 expected
+    # an F32 linear weight is refused like loader.rs:131-134
+    real = write_gguf.should_quantize
+    monkeypatch.setattr(write_gguf, "should_quantize",
+                        lambda n, s: False if n == "encoder.blocks.0.attn.query.weight" else real(n, s))
+    q = tmp_path / "f32.gguf"
+    write_gguf.write_gguf(str(q), tensors, "t")
+    with pytest.raises(wq4.WQ4Error, match="Expected Q4_0 for weight 'encoder.blocks.0.attn.query.weight'"):
+        whisper_amd.WhisperModel.from_gguf(str(q), "tiny_test", max_batch=1)
+    monkeypatch.undo()
+    del tensors["decoder.ln.bias"]
+    r = tmp_path / "missing.gguf"
+    write_gguf.write_gguf(str(r), tensors, "t")
+    with pytest.raises(wq4.WQ4Error, match="Tensor 'decoder.ln.bias' not found"):
+        whisper_amd.WhisperModel.from_gguf(str(r), "tiny_test", max_batch=1)

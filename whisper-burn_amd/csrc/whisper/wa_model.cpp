@@ -29,6 +29,7 @@
 
 #include "../../../include/whisper_amd.h"
 #include "../../../include/wq4.h"
+#include "wa_gguf.hpp"
 #include "wa_kernels.hpp"
 
 namespace {
@@ -234,9 +235,87 @@ struct wa_model {
 
 namespace {
 
+// Where the weights come from: the synthetic generator (no checkpoint is
+// available offline) or a GGUF file (loader.rs).  Names are the GGUF names.
+struct Source {
+  virtual ~Source() = default;
+  // n f32 values of `name`; false (no error) when an optional tensor is absent
+  virtual bool f32(const std::string& name, int64_t n, float lo, float hi, bool optional, std::vector<float>& out) = 0;
+  // raw Q4_0 bytes of the [rows, k] weight `name` written at dst
+  virtual bool q4(const std::string& name, int rows, int k, uint8_t* dst) = 0;
+  std::string err;
+};
+
+struct SynthSource : Source {
+  uint64_t seed;
+  explicit SynthSource(uint64_t s) : seed(s) {}
+  bool f32(const std::string& name, int64_t n, float lo, float hi, bool optional, std::vector<float>& out) override {
+    // Whisper's attention key projections have no bias (loader.rs:205-210)
+    if (optional && name.size() > 9 && name.compare(name.size() - 9, 9, ".key.bias") == 0) return false;
+    out.resize((size_t)n);
+    synth_uniform(seed, name, n, lo, hi, out.data());
+    return true;
+  }
+  bool q4(const std::string& name, int rows, int k, uint8_t* dst) override {
+    std::vector<float> w((size_t)rows * k);
+    synth_uniform(seed, name, (int64_t)rows * k, -lin_scale(k), lin_scale(k), w.data());
+    const int64_t nblk = (int64_t)rows * k / 32;
+    parallel_for(nblk, [&](int64_t a, int64_t b) {
+      (void)wq4_quantize_q4_0(w.data() + a * 32, (b - a) * 32, dst + a * 18);
+    });
+    return true;
+  }
+};
+
+// f16 (IEEE binary16, little-endian) -> f32, exact (half 2.7.1 semantics).
+float f16_to_f32(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+
+struct GgufSource : Source {
+  const wa::GgufFile& g;
+  explicit GgufSource(const wa::GgufFile& f) : g(f) {}
+  bool bad(const std::string& m) {
+    err = m;
+    return false;
+  }
+  // loader.rs:47-104 (F32 / F16 1-D and 2-D tensors, 3-D conv weights)
+  bool f32(const std::string& name, int64_t n, float, float, bool optional, std::vector<float>& out) override {
+    const wa::GgufTensor* t = g.find(name);
+    if (!t) return optional ? false : bad("Tensor '" + name + "' not found");
+    if (t->type != wa::kGgmlF32 && t->type != wa::kGgmlF16)
+      return bad("Expected F32/F16 for '" + name + "', got Q4_0");
+    if ((int64_t)t->elements() != n)
+      return bad("Tensor '" + name + "' has " + std::to_string(t->elements()) + " elements, expected " +
+                 std::to_string(n));
+    const uint8_t* p = g.data(*t);
+    if (!p) return bad("Tensor '" + name + "' data lies outside the file");
+    out.resize((size_t)n);
+    if (t->type == wa::kGgmlF32) {
+      std::memcpy(out.data(), p, (size_t)n * 4);
+    } else {
+      for (int64_t i = 0; i < n; ++i) out[(size_t)i] = f16_to_f32((uint16_t)(p[2 * i] | (p[2 * i + 1] << 8)));
+    }
+    return true;
+  }
+  // loader.rs:106-144: Q4_0 only; GGUF dims are [in_features, out_features]
+  bool q4(const std::string& name, int rows, int k, uint8_t* dst) override {
+    const wa::GgufTensor* t = g.find(name);
+    if (!t) return bad("Tensor '" + name + "' not found");
+    if (t->type != wa::kGgmlQ4_0)
+      return bad("Expected Q4_0 for weight '" + name + "', got " + (t->type == wa::kGgmlF32 ? "F32" : "F16") +
+                 ". Use the conversion script.");
+    if (t->dims.size() != 2 || t->dims[0] != (uint64_t)k || t->dims[1] != (uint64_t)rows)
+      return bad("Q4 weight '" + name + "' has the wrong shape (expected [" + std::to_string(rows) + ", " +
+                 std::to_string(k) + "])");
+    const uint8_t* p = g.data(*t);
+    if (!p) return bad("Tensor '" + name + "' data lies outside the file");
+    std::memcpy(dst, p, t->nbytes());
+    return true;
+  }
+};
+
 struct Builder {
   wa_model* m;
-  uint64_t seed;
+  Source& src;
   wq4_status st = WQ4_OK;
 
   float* upload(const std::vector<float>& v) {
@@ -248,25 +327,26 @@ struct Builder {
     m->bytes += v.size() * 4;
     return p;
   }
-  std::vector<float> gen(const std::string& name, int64_t n, float lo, float hi) {
-    std::vector<float> v((size_t)n);
-    synth_uniform(seed, name, n, lo, hi, v.data());
+  std::vector<float> get(const std::string& name, int64_t n, float lo, float hi) {
+    std::vector<float> v;
+    if (st == WQ4_OK && !src.f32(name, n, lo, hi, false, v)) st = fail(WQ4_EINVAL, src.err);
+    if (v.size() != (size_t)n) v.assign((size_t)n, 0.0f);
     return v;
   }
-  float* vec(const std::string& name, int64_t n, float lo, float hi) { return upload(gen(name, n, lo, hi)); }
-  // Q4 weights of several GGUF tensors [n_i, k], row-concatenated.
+  float* vec(const std::string& name, int64_t n, float lo, float hi) { return upload(get(name, n, lo, hi)); }
+  // Q4 weights of several GGUF tensors [n_i, k], row-concatenated (a fused projection).
   wq4_tensor* q4(const std::vector<std::string>& names, const std::vector<int>& rows, int k) {
+    if (st != WQ4_OK) return nullptr;
     int64_t total = 0;
     for (int r : rows) total += r;
     std::vector<uint8_t> raw((size_t)(total * k / 32 * 18));
     size_t off = 0;
     for (size_t i = 0; i < names.size(); ++i) {
-      std::vector<float> w = gen(names[i], (int64_t)rows[i] * k, -lin_scale(k), lin_scale(k));
-      const int64_t nblk = (int64_t)rows[i] * k / 32;
-      parallel_for(nblk, [&](int64_t a, int64_t b) {
-        (void)wq4_quantize_q4_0(w.data() + a * 32, (b - a) * 32, raw.data() + off + a * 18);
-      });
-      off += (size_t)nblk * 18;
+      if (!src.q4(names[i], rows[i], k, raw.data() + off)) {
+        st = fail(WQ4_EINVAL, src.err);
+        return nullptr;
+      }
+      off += (size_t)rows[i] * k / 32 * 18;
     }
     wq4_tensor* t = nullptr;
     wq4_status s = wq4_tensor_create(m->device, raw.data(), raw.size(), total, k, &t);
@@ -278,18 +358,20 @@ struct Builder {
   float* bias_cat(const std::vector<std::string>& names, int n) {
     std::vector<float> v;
     for (const auto& nm : names) {
-      if (nm.empty()) {
-        v.insert(v.end(), n, 0.0f);
-      } else {
-        auto b = gen(nm, n, -0.02f, 0.02f);
+      std::vector<float> b;
+      if (st == WQ4_OK && src.f32(nm, n, -0.02f, 0.02f, true, b)) {
         v.insert(v.end(), b.begin(), b.end());
+      } else {
+        if (!src.err.empty()) st = fail(WQ4_EINVAL, src.err);
+        v.insert(v.end(), n, 0.0f);
       }
     }
     return upload(v);
   }
-  // conv weight [N, C, 3] -> [N][kk*C + c] (im2col order, layers.rs:118-121)
+  // conv weight [N, C, 3] (GGUF dims [3, C, N], loader.rs:254-268) ->
+  // [N][kk*C + c] (im2col order, layers.rs:118-121)
   float* conv(const std::string& name, int N, int C) {
-    auto w = gen(name, (int64_t)N * C * 3, -lin_scale(3 * C), lin_scale(3 * C));
+    auto w = get(name, (int64_t)N * C * 3, -lin_scale(3 * C), lin_scale(3 * C));
     std::vector<float> t((size_t)N * 3 * C);
     for (int n = 0; n < N; ++n)
       for (int c = 0; c < C; ++c)
@@ -298,10 +380,11 @@ struct Builder {
   }
 };
 
-wq4_status build_synthetic(wa_model* m, uint64_t seed) {
+// Every weight of the model (loader.rs:279-377 load_encoder / load_decoder).
+wq4_status build_model(wa_model* m, Source& src) {
   const Config& c = m->cfg;
   const int D = c.n_audio_state, F = 4 * D, Dt = c.n_text_state, Ft = 4 * Dt;
-  Builder B{m, seed};
+  Builder B{m, src};
   m->conv1_wt = B.conv("encoder.conv1.weight", D, c.n_mels);
   m->conv1_b = B.vec("encoder.conv1.bias", D, -0.02f, 0.02f);
   m->conv2_wt = B.conv("encoder.conv2.weight", D, D);
@@ -314,7 +397,7 @@ wq4_status build_synthetic(wa_model* m, uint64_t seed) {
     L.ln1_w = B.vec(p + ".attn_ln.weight", D, 0.9f, 1.1f);
     L.ln1_b = B.vec(p + ".attn_ln.bias", D, -0.05f, 0.05f);
     L.qkv = B.q4({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, {D, D, D}, D);
-    L.qkv_b = B.bias_cat({p + ".attn.query.bias", "", p + ".attn.value.bias"}, D);
+    L.qkv_b = B.bias_cat({p + ".attn.query.bias", p + ".attn.key.bias", p + ".attn.value.bias"}, D);
     L.out = B.q4({p + ".attn.out.weight"}, {D}, D);
     L.out_b = B.vec(p + ".attn.out.bias", D, -0.02f, 0.02f);
     L.ln2_w = B.vec(p + ".mlp_ln.weight", D, 0.9f, 1.1f);
@@ -336,7 +419,7 @@ wq4_status build_synthetic(wa_model* m, uint64_t seed) {
     L.ln1_w = B.vec(p + ".attn_ln.weight", Dt, 0.9f, 1.1f);
     L.ln1_b = B.vec(p + ".attn_ln.bias", Dt, -0.05f, 0.05f);
     L.qkv = B.q4({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, {Dt, Dt, Dt}, Dt);
-    L.qkv_b = B.bias_cat({p + ".attn.query.bias", "", p + ".attn.value.bias"}, Dt);
+    L.qkv_b = B.bias_cat({p + ".attn.query.bias", p + ".attn.key.bias", p + ".attn.value.bias"}, Dt);
     L.out = B.q4({p + ".attn.out.weight"}, {Dt}, Dt);
     L.out_b = B.vec(p + ".attn.out.bias", Dt, -0.02f, 0.02f);
     L.ln2_w = B.vec(p + ".cross_attn_ln.weight", Dt, 0.9f, 1.1f);
@@ -345,7 +428,7 @@ wq4_status build_synthetic(wa_model* m, uint64_t seed) {
     L.cq_b = B.vec(p + ".cross_attn.query.bias", Dt, -0.02f, 0.02f);
     // cross-attention key has no bias (loader.rs:205-210)
     L.ckv = B.q4({p + ".cross_attn.key.weight", p + ".cross_attn.value.weight"}, {Dt, Dt}, D);
-    L.ckv_b = B.bias_cat({"", p + ".cross_attn.value.bias"}, Dt);
+    L.ckv_b = B.bias_cat({p + ".cross_attn.key.bias", p + ".cross_attn.value.bias"}, Dt);
     L.cout = B.q4({p + ".cross_attn.out.weight"}, {Dt}, Dt);
     L.cout_b = B.vec(p + ".cross_attn.out.bias", Dt, -0.02f, 0.02f);
     L.ln3_w = B.vec(p + ".mlp_ln.weight", Dt, 0.9f, 1.1f);
@@ -686,7 +769,35 @@ wq4_status wa_model_create_synthetic(int device, int variant, uint64_t seed, int
   m->prec = prec;
   m->ns = prec == WQ4_PREC_F16 ? 1 : 2;
   m->bmax = max_batch;
-  wq4_status s = build_synthetic(m.get(), seed);
+  SynthSource src(seed);
+  wq4_status s = build_model(m.get(), src);
+  if (s != WQ4_OK) return s;
+  s = alloc_activations(m.get());
+  if (s != WQ4_OK) return s;
+  WA_HIP(hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking));
+  WA_HIP(hipDeviceSynchronize());
+  *out = m.release();
+  return WQ4_OK;
+}
+
+wq4_status wa_model_create_from_gguf(int device, const char* path, int variant, int max_batch, wq4_precision prec,
+                                     wa_model** out) {
+  if (!out || !path) return fail(WQ4_EINVAL, "null argument");
+  *out = nullptr;
+  if (variant < 0 || variant > 2) return fail(WQ4_EINVAL, "unknown variant");
+  if (max_batch < 1 || max_batch > 256) return fail(WQ4_EINVAL, "max_batch must be in [1, 256]");
+  if (prec != WQ4_PREC_F16X2 && prec != WQ4_PREC_F16) return fail(WQ4_EINVAL, "unknown precision");
+  wa::GgufFile file;
+  if (!file.open(path)) return fail(WQ4_EINVAL, "Failed to parse GGUF: " + file.error());
+  WA_HIP(hipSetDevice(device));
+  std::unique_ptr<wa_model> m(new wa_model());
+  m->device = device;
+  m->cfg = preset(variant);
+  m->prec = prec;
+  m->ns = prec == WQ4_PREC_F16 ? 1 : 2;
+  m->bmax = max_batch;
+  GgufSource src(file);
+  wq4_status s = build_model(m.get(), src);
   if (s != WQ4_OK) return s;
   s = alloc_activations(m.get());
   if (s != WQ4_OK) return s;
@@ -697,6 +808,59 @@ wq4_status wa_model_create_synthetic(int device, int variant, uint64_t seed, int
 }
 
 void wa_model_destroy(wa_model* m) { delete m; }
+
+wq4_status wa_gguf_open(const char* path, wa_gguf** out) {
+  if (!path || !out) return fail(WQ4_EINVAL, "null argument");
+  *out = nullptr;
+  auto* f = new wa::GgufFile();
+  if (!f->open(path)) {
+    const std::string e = f->error();
+    delete f;
+    return fail(WQ4_EINVAL, "Failed to parse GGUF: " + e);
+  }
+  *out = reinterpret_cast<wa_gguf*>(f);
+  return WQ4_OK;
+}
+
+void wa_gguf_close(wa_gguf* g) { delete reinterpret_cast<wa::GgufFile*>(g); }
+
+int wa_gguf_version(const wa_gguf* g) { return g ? (int)reinterpret_cast<const wa::GgufFile*>(g)->version() : -1; }
+
+int64_t wa_gguf_tensor_count(const wa_gguf* g) {
+  return g ? (int64_t)reinterpret_cast<const wa::GgufFile*>(g)->tensors().size() : -1;
+}
+
+wq4_status wa_gguf_tensor_info(const wa_gguf* g, int64_t index, char* name, size_t name_cap, int* ndims,
+                               uint64_t* dims, int* type, uint64_t* offset, uint64_t* nbytes) {
+  if (!g) return fail(WQ4_EINVAL, "null gguf");
+  const auto& ts = reinterpret_cast<const wa::GgufFile*>(g)->tensors();
+  if (index < 0 || index >= (int64_t)ts.size()) return fail(WQ4_EINVAL, "tensor index out of range");
+  const wa::GgufTensor& t = ts[(size_t)index];
+  if (name && name_cap) {
+    const size_t n = std::min(name_cap - 1, t.name.size());
+    std::memcpy(name, t.name.data(), n);
+    name[n] = 0;
+  }
+  if (ndims) *ndims = (int)t.dims.size();
+  if (dims)
+    for (size_t i = 0; i < t.dims.size(); ++i) dims[i] = t.dims[i];
+  if (type) *type = (int)t.type;
+  if (offset) *offset = t.offset;
+  if (nbytes) *nbytes = t.nbytes();
+  return WQ4_OK;
+}
+
+wq4_status wa_gguf_tensor_data(const wa_gguf* g, const char* name, uint8_t* out, size_t cap) {
+  if (!g || !name || !out) return fail(WQ4_EINVAL, "null argument");
+  const auto* f = reinterpret_cast<const wa::GgufFile*>(g);
+  const wa::GgufTensor* t = f->find(name);
+  if (!t) return fail(WQ4_EINVAL, std::string("Tensor '") + name + "' not found in GGUF");
+  const uint8_t* p = f->data(*t);
+  if (!p) return fail(WQ4_EINVAL, std::string("Tensor '") + name + "' data lies outside the file");
+  if (cap < t->nbytes()) return fail(WQ4_ENOMEM, "output buffer too small");
+  std::memcpy(out, p, t->nbytes());
+  return WQ4_OK;
+}
 
 wq4_status wa_model_config(const wa_model* m, int32_t* cfg) {
   if (!m || !cfg) return fail(WQ4_EINVAL, "null argument");

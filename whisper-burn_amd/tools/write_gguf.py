@@ -1,0 +1,178 @@
+"""GGUF writer: the on-disk format of scripts/convert_whisper.py, and a
+synthetic Whisper checkpoint in it.
+
+    python whisper-burn_amd/tools/write_gguf.py --variant tiny_test --seed 1234 --out /tmp/tiny.gguf
+
+write_gguf() lays a file out exactly like the reference converter
+(convert_whisper.py:138-214): tensors sorted by name, dims reversed,
+should_quantize() picks Q4_0 (else F32), data offsets 32-byte aligned, the
+four metadata keys, data section at the next 32-byte boundary.  The bytes are
+pinned by tests/golden/ref_writer_tiny.gguf (written with the reference's own
+helpers).  synthetic_tensors() yields the same weights as
+wa_model_create_synthetic (same generator, names, ranges and quantizer), so a
+model loaded from the file equals the synthetic model bit for bit.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import struct
+import sys
+from typing import Iterator
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+GGUF_MAGIC = 0x46554747
+GGUF_VERSION = 3
+ALIGNMENT = 32
+GGML_F32, GGML_F16, GGML_Q4_0 = 0, 1, 2
+
+CONFIGS = {  # src/model/config.rs:32-63 (+ the 2+2-layer parity-test size)
+    "large_v3": dict(n_mels=128, n_audio_ctx=1500, n_audio_state=1280, n_audio_layer=32, n_text_ctx=448,
+                     n_text_state=1280, n_text_layer=32, n_vocab=51866),
+    "medium": dict(n_mels=80, n_audio_ctx=1500, n_audio_state=1024, n_audio_layer=24, n_text_ctx=448,
+                   n_text_state=1024, n_text_layer=24, n_vocab=51865),
+    "tiny_test": dict(n_mels=80, n_audio_ctx=1500, n_audio_state=384, n_audio_layer=2, n_text_ctx=448,
+                      n_text_state=384, n_text_layer=2, n_vocab=51866),
+}
+
+
+def should_quantize(name: str, shape: tuple) -> bool:
+    """convert_whisper.py:76-95: 2-D, min dim >= 256, not bias/LN/embedding/conv."""
+    if len(shape) != 2 or min(shape) < 256:
+        return False
+    return not any(s in name for s in ("bias", "ln", "layer_norm", "positional_embedding", "token_embedding",
+                                       "conv"))
+
+
+def _gguf_string(s: str) -> bytes:
+    b = s.encode("utf-8")
+    return struct.pack("<Q", len(b)) + b
+
+
+def _align(off: int) -> int:
+    return (off + ALIGNMENT - 1) // ALIGNMENT * ALIGNMENT
+
+
+def write_gguf(path: str, tensors: dict[str, np.ndarray], model_name: str, quantize=None) -> None:
+    """tensors: GGUF name -> f32 array (PyTorch shape).  quantize(array) ->
+    Q4_0 bytes (default: wq4.quantize_q4_0, the product quantizer)."""
+    if quantize is None:
+        import wq4
+
+        quantize = wq4.quantize_q4_0
+    entries, blobs, cur = [], [], 0
+    for name in sorted(tensors):
+        a = np.asarray(tensors[name], np.float32)
+        if should_quantize(name, a.shape):
+            data, dtype = bytes(quantize(a)), GGML_Q4_0
+        else:
+            data, dtype = a.astype(np.float32).tobytes(), GGML_F32
+        off = _align(cur)
+        entries.append((name, list(reversed(a.shape)), dtype, off))
+        blobs.append((off - cur, data))
+        cur = off + len(data)
+    enc = len([n for n in tensors if n.startswith("encoder.blocks.")]) // 8
+    dec = len([n for n in tensors if n.startswith("decoder.blocks.")]) // 16
+    meta = [("general.architecture", 8, "whisper"), ("general.name", 8, model_name),
+            ("whisper.encoder.layer_count", 4, enc), ("whisper.decoder.layer_count", 4, dec)]
+    with open(path, "wb") as f:
+        f.write(struct.pack("<IIQQ", GGUF_MAGIC, GGUF_VERSION, len(entries), len(meta)))
+        for key, vt, val in meta:
+            f.write(_gguf_string(key) + struct.pack("<I", vt))
+            f.write(struct.pack("<I", val) if vt == 4 else _gguf_string(val))
+        for name, dims, dtype, off in entries:
+            f.write(_gguf_string(name) + struct.pack("<I", len(dims)))
+            f.write(b"".join(struct.pack("<Q", d) for d in dims))
+            f.write(struct.pack("<IQ", dtype, off))
+        pos = f.tell()
+        f.write(b"\x00" * (_align(pos) - pos))
+        for pad, data in blobs:
+            f.write(b"\x00" * pad)
+            f.write(data)
+
+
+def _lin(k: int) -> float:
+    return float(np.float32(1.5 / np.sqrt(k)))
+
+
+def synthetic_specs(variant: str) -> Iterator[tuple[str, tuple, float, float]]:
+    """(GGUF name, PyTorch shape, lo, hi) of every tensor of the synthetic
+    model -- the table wa_model.cpp build_model() draws from."""
+    c = CONFIGS[variant]
+    D, T, M = c["n_audio_state"], c["n_audio_ctx"], c["n_mels"]
+    Dt = c["n_text_state"]
+
+    def ln(p, n):
+        yield f"{p}.weight", (n,), 0.9, 1.1
+        yield f"{p}.bias", (n,), -0.05, 0.05
+
+    def lin(p, n, k, bias=True):
+        yield f"{p}.weight", (n, k), -_lin(k), _lin(k)
+        if bias:
+            yield f"{p}.bias", (n,), -0.02, 0.02
+
+    yield "encoder.conv1.weight", (D, M, 3), -_lin(3 * M), _lin(3 * M)
+    yield "encoder.conv1.bias", (D,), -0.02, 0.02
+    yield "encoder.conv2.weight", (D, D, 3), -_lin(3 * D), _lin(3 * D)
+    yield "encoder.conv2.bias", (D,), -0.02, 0.02
+    yield "encoder.positional_embedding", (T, D), -0.1, 0.1
+    for i in range(c["n_audio_layer"]):
+        p = f"encoder.blocks.{i}"
+        yield from ln(f"{p}.attn_ln", D)
+        yield from lin(f"{p}.attn.query", D, D)
+        yield from lin(f"{p}.attn.key", D, D, bias=False)
+        yield from lin(f"{p}.attn.value", D, D)
+        yield from lin(f"{p}.attn.out", D, D)
+        yield from ln(f"{p}.mlp_ln", D)
+        yield from lin(f"{p}.mlp.0", 4 * D, D)
+        yield from lin(f"{p}.mlp.2", D, 4 * D)
+    yield from ln("encoder.ln_post", D)
+    yield "decoder.token_embedding.weight", (c["n_vocab"], Dt), -_lin(Dt), _lin(Dt)
+    yield "decoder.positional_embedding", (c["n_text_ctx"], Dt), -0.02, 0.02
+    for i in range(c["n_text_layer"]):
+        p = f"decoder.blocks.{i}"
+        yield from ln(f"{p}.attn_ln", Dt)
+        yield from lin(f"{p}.attn.query", Dt, Dt)
+        yield from lin(f"{p}.attn.key", Dt, Dt, bias=False)
+        yield from lin(f"{p}.attn.value", Dt, Dt)
+        yield from lin(f"{p}.attn.out", Dt, Dt)
+        yield from ln(f"{p}.cross_attn_ln", Dt)
+        yield from lin(f"{p}.cross_attn.query", Dt, Dt)
+        yield from lin(f"{p}.cross_attn.key", Dt, D, bias=False)
+        yield from lin(f"{p}.cross_attn.value", Dt, D)
+        yield from lin(f"{p}.cross_attn.out", Dt, Dt)
+        yield from ln(f"{p}.mlp_ln", Dt)
+        yield from lin(f"{p}.mlp.0", 4 * Dt, Dt)
+        yield from lin(f"{p}.mlp.2", Dt, 4 * Dt)
+    yield from ln("decoder.ln", Dt)
+
+
+def synthetic_tensors(variant: str, seed: int) -> dict[str, np.ndarray]:
+    import whisper_amd
+
+    out = {}
+    for name, shape, lo, hi in synthetic_specs(variant):
+        out[name] = whisper_amd.synth_uniform(seed, name, int(np.prod(shape)), lo, hi).reshape(shape)
+    return out
+
+
+def write_synthetic_gguf(path: str, variant: str, seed: int) -> None:
+    write_gguf(path, synthetic_tensors(variant, seed), f"synthetic-whisper-{variant}-seed{seed}")
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variant", default="tiny_test", choices=sorted(CONFIGS))
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    write_synthetic_gguf(a.out, a.variant, a.seed)
+    print(f"wrote {a.out} ({os.path.getsize(a.out) / 2**20:.1f} MiB)")
+
+
+if __name__ == "__main__":
+    main()

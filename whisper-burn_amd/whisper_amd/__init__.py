@@ -47,8 +47,21 @@ def lib() -> ctypes.CDLL:
         L.wa_profile_enable.argtypes = [vp, c_int]
         L.wa_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), c_int]
         L.wa_probe_kernels.argtypes = [vp, c_int, c_int, ctypes.POINTER(ctypes.c_double)]
+        L.wa_model_create_from_gguf.argtypes = [c_int, ctypes.c_char_p, c_int, c_int, c_int, ctypes.POINTER(vp)]
+        L.wa_gguf_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
+        L.wa_gguf_close.argtypes = [vp]
+        L.wa_gguf_close.restype = None
+        L.wa_gguf_version.argtypes = [vp]
+        L.wa_gguf_version.restype = c_int
+        L.wa_gguf_tensor_count.argtypes = [vp]
+        L.wa_gguf_tensor_count.restype = c_i64
+        L.wa_gguf_tensor_info.argtypes = [vp, c_i64, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(c_int),
+                                          ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(c_int),
+                                          ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.wa_gguf_tensor_data.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t]
         for n in ("wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
-                  "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read", "wa_probe_kernels"):
+                  "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read", "wa_probe_kernels",
+                  "wa_model_create_from_gguf", "wa_gguf_open", "wa_gguf_tensor_info", "wa_gguf_tensor_data"):
             getattr(L, n).restype = c_int
         _lib = L
     return _lib
@@ -71,14 +84,64 @@ def _torch():
     return torch
 
 
+class GgufReader:
+    """GgufReader (src/gguf/reader.rs): header, tensor index, tensor bytes."""
+
+    def __init__(self, path: str):
+        h = ctypes.c_void_p(None)
+        check(lib().wa_gguf_open(path.encode(), ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def version(self) -> int:
+        return lib().wa_gguf_version(self._h)
+
+    def tensors(self) -> list[dict]:
+        """File-order tensor index: name, dims (GGUF order), type, offset, nbytes."""
+        out = []
+        for i in range(lib().wa_gguf_tensor_count(self._h)):
+            name = ctypes.create_string_buffer(512)
+            nd, ty = ctypes.c_int(), ctypes.c_int()
+            dims = (ctypes.c_uint64 * 8)()
+            off, nb = ctypes.c_uint64(), ctypes.c_uint64()
+            check(lib().wa_gguf_tensor_info(self._h, i, name, 512, ctypes.byref(nd), dims, ctypes.byref(ty),
+                                            ctypes.byref(off), ctypes.byref(nb)))
+            out.append({"name": name.value.decode(), "dims": list(dims[: nd.value]), "type": ty.value,
+                        "offset": off.value, "nbytes": nb.value})
+        return out
+
+    def tensor_data(self, name: str) -> np.ndarray:
+        info = next(t for t in self.tensors() if t["name"] == name)
+        buf = np.empty(info["nbytes"], np.uint8)
+        check(lib().wa_gguf_tensor_data(self._h, name.encode(), buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                         buf.size))
+        return buf
+
+    def close(self):
+        if self._h and self._h.value:
+            lib().wa_gguf_close(self._h)
+            self._h = ctypes.c_void_p(None)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class WhisperModel:
-    """A Whisper model with synthetic weights resident on one MI355X."""
+    """A Whisper model resident on one MI355X: synthetic weights (default) or
+    a GGUF checkpoint (WhisperModel.from_gguf, src/gguf/loader.rs)."""
 
     def __init__(self, variant: str = "large_v3", seed: int = 1234, max_batch: int = 1, device: int = 0,
-                 precision: int = wq4.PREC_F16X2):
+                 precision: int = wq4.PREC_F16X2, gguf_path: Optional[str] = None):
         h = ctypes.c_void_p(None)
-        check(lib().wa_model_create_synthetic(device, VARIANTS[variant], seed, max_batch, precision,
-                                              ctypes.byref(h)))
+        if gguf_path is None:
+            check(lib().wa_model_create_synthetic(device, VARIANTS[variant], seed, max_batch, precision,
+                                                  ctypes.byref(h)))
+        else:
+            check(lib().wa_model_create_from_gguf(device, gguf_path.encode(), VARIANTS[variant], max_batch,
+                                                  precision, ctypes.byref(h)))
         self._h = h
         self.device = device
         self.variant = variant
@@ -86,6 +149,12 @@ class WhisperModel:
         cfg = (ctypes.c_int32 * len(CFG_KEYS))()
         check(lib().wa_model_config(h, cfg))
         self.config = dict(zip(CFG_KEYS, list(cfg)))
+
+    @classmethod
+    def from_gguf(cls, path: str, variant: str = "large_v3", max_batch: int = 1, device: int = 0,
+                  precision: int = wq4.PREC_F16X2) -> "WhisperModel":
+        """load_whisper_from_gguf (src/gguf/loader.rs:26-45)."""
+        return cls(variant, 0, max_batch, device, precision, gguf_path=path)
 
     def device_bytes(self) -> int:
         return int(lib().wa_model_device_bytes(self._h))

@@ -73,6 +73,7 @@ def _declare(L: ctypes.CDLL) -> None:
     L.wq4_linear_forward_ws.argtypes = [vp, vp, vp, vp, vp, c_i64, c_i64, ctypes.c_uint, c_int, vp, c_sz, vp]
     L.wq4_ffn_forward_ws.argtypes = [vp, vp, vp, vp, vp, vp, vp, c_i64, ctypes.c_uint, c_int, vp, c_sz, vp]
     L.wq4_debug_repack.argtypes = [u8p, c_i64, c_i64, u8p, ctypes.POINTER(ctypes.c_uint32), f32p]
+    L.wq4_quantize_q4_0.argtypes = [f32p, c_i64, u8p]
     L.wq4_debug_unrepack.argtypes = [u8p, ctypes.POINTER(ctypes.c_uint32), f32p, c_i64, c_i64, u8p]
     L.wq4_debug_repacked_bytes.argtypes = [c_i64, c_i64, ctypes.POINTER(c_sz), ctypes.POINTER(c_sz),
                                            ctypes.POINTER(c_sz)]
@@ -91,7 +92,7 @@ def _declare(L: ctypes.CDLL) -> None:
     for name in ("wq4_device_count", "wq4_set_precision", "wq4_set_kernel_policy", "wq4_tensor_create",
                  "wq4_tensor_shape", "wq4_tensor_dequantize", "wq4_tensor_raw_bytes", "wq4_matmul",
                  "wq4_linear_forward", "wq4_ffn_forward", "wq4_linear_forward_ws", "wq4_ffn_forward_ws",
-                 "wq4_debug_repack", "wq4_debug_unrepack", "wq4_debug_repacked_bytes"):
+                 "wq4_debug_repack", "wq4_debug_unrepack", "wq4_debug_repacked_bytes", "wq4_quantize_q4_0"):
         getattr(L, name).restype = c_int
 
 
@@ -144,6 +145,14 @@ def _u8p(a: np.ndarray):
 
 def _f32p(a: np.ndarray):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def quantize_q4_0(x: np.ndarray) -> np.ndarray:
+    """Q4_0 bytes of f32 values (scripts/convert_whisper.py:33-74 semantics)."""
+    x = np.ascontiguousarray(x, dtype=np.float32).ravel()
+    out = np.empty(x.size // 32 * 18, np.uint8)
+    check(lib().wq4_quantize_q4_0(_f32p(x), x.size, _u8p(out)))
+    return out
 
 
 def debug_repack(raw: np.ndarray, n: int, k: int) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
