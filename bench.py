@@ -125,6 +125,8 @@ def main() -> None:
     ap.add_argument("--max-tokens", type=int, default=224)
     ap.add_argument("--lang", type=int, default=50259, help="language token; -1 = auto-detect")
     ap.add_argument("--precision", default="f16x2", choices=["f16x2", "f16"])
+    ap.add_argument("--weights", default="q4_0", choices=["q4_0", "f16"],
+                    help="linear weights: Q4_0 (default) or unquantized f16 (BASELINE config 5)")
     ap.add_argument("--fixed-length", action="store_true", help="ignore EOT (always max-tokens steps)")
     ap.add_argument("--cpu-rows", type=int, default=750)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -150,7 +152,7 @@ def main() -> None:
     prec = wq4.PREC_F16X2 if args.precision == "f16x2" else wq4.PREC_F16
     t_load = time.perf_counter()
     model = whisper_amd.WhisperModel(args.variant, args.seed, max_batch=args.clips_per_gpu, device=local_rank,
-                                     precision=prec)
+                                     precision=prec, weights=args.weights)
     t_load = time.perf_counter() - t_load
     cfg = model.config
     B = args.clips_per_gpu
@@ -219,10 +221,10 @@ def main() -> None:
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp16x2" if prec == wq4.PREC_F16X2 else "fp16", "data": "synthetic",
-            "config": {"workload": f"Whisper {args.variant} Q4_0, {B} synthetic 30-s clips per GPU per step "
+            "config": {"workload": f"Whisper {args.variant} {args.weights.upper()}, {B} synthetic 30-s clips per GPU per step "
                                    f"(BASELINE config 4 shard), greedy KV-cached decode, max {args.max_tokens} "
                                    f"tokens, {'fixed length' if args.fixed_length else 'EOT stop'}",
-                       "model": f"whisper-{args.variant.replace('_', '-')}-q4_0 (synthetic weights)",
+                       "model": f"whisper-{args.variant.replace('_', '-')}-{args.weights} (synthetic weights)",
                        "global_batch": clips // args.steps, "seq_len": cfg["n_audio_ctx"],
                        "parallelism": f"replicas{world} (independent clips, no collectives)"},
             "roofline": dominant,

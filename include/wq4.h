@@ -80,6 +80,15 @@ wq4_precision wq4_get_precision(void);
 wq4_status wq4_tensor_create(int device, const uint8_t* raw, size_t nbytes, int64_t n, int64_t k,
                              wq4_tensor** out);
 void wq4_tensor_destroy(wq4_tensor* t);
+/* Unquantized weights (BASELINE config 5; GGUF F16 linear tensors, which the
+ * reference loader rejects, loader.rs:131-134): w = host IEEE halves [N, K]
+ * row-major, K % 32 == 0.  The same GEMM entry points then run the MFMA
+ * kernels on the f16 weights directly (x = hi + lo against the exact f16 w:
+ * two MFMA passes instead of three).  dequantize() returns the f16 values
+ * as f32; raw_bytes() the 2*N*K bytes as given. */
+wq4_status wq4_tensor_create_f16(int device, const uint16_t* w, int64_t n, int64_t k, wq4_tensor** out);
+/* 0 = Q4_0 blocks, 1 = f16 weights. */
+int wq4_tensor_weight_type(const wq4_tensor* t);
 /* Q4Tensor::shape (tensor.rs:74-76): [N, K]. */
 wq4_status wq4_tensor_shape(const wq4_tensor* t, int64_t* n, int64_t* k);
 /* Q4Tensor::num_blocks (tensor.rs:79-81). */

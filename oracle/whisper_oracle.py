@@ -49,10 +49,11 @@ def synthetic_mel(clip: int, n_mels: int, seed: int = 0x5EED0000) -> np.ndarray:
 
 
 class SynthWhisper:
-    def __init__(self, variant: str = "tiny_test", seed: int = 1234, dtype=np.float32):
+    def __init__(self, variant: str = "tiny_test", seed: int = 1234, dtype=np.float32, weights: str = "q4_0"):
         self.cfg = dict(CONFIGS[variant])
         self.seed = seed
         self.dt = dtype
+        self.weights = weights  # "q4_0", or "f16" (BASELINE config 5: linear weights rounded to f16)
         self.w: dict[str, np.ndarray] = {}
         self._build()
 
@@ -62,6 +63,8 @@ class SynthWhisper:
 
     def _q4(self, name, n, k):
         a = float(oracle.lin_scale(k))
+        if self.weights == "f16":
+            return self._u(name, n * k, -a, a).astype(np.float16).reshape(n, k).astype(self.dt)
         q = oracle.quantize_convert_np(self._u(name, n * k, -a, a))
         return oracle.dequantize_np(q, n * k).reshape(n, k).astype(self.dt)
 

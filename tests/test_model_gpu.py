@@ -138,3 +138,35 @@ def test_gguf_loader_errors(torch, tmp_path, monkeypatch):
     write_gguf.write_gguf(str(r), tensors, "t")
     with pytest.raises(wq4.WQ4Error, match="Tensor 'decoder.ln.bias' not found"):
         whisper_amd.WhisperModel.from_gguf(str(r), "tiny_test", max_batch=1)
+
+
+# ------------------------------------------- f16 weights (BASELINE config 5) --
+def test_f16_weight_model_matches_oracle(torch):
+    """Config 5's unquantized path: linear weights f16 (the synthetic values
+    rounded to f16), same kernels; tokens equal to the oracle run on the same
+    f16 weights, and a GGUF F16 checkpoint loads to the same model."""
+    import whisper_amd
+
+    ref = wo.SynthWhisper("tiny_test", SEED, weights="f16")
+    gm = whisper_amd.WhisperModel("tiny_test", SEED, max_batch=2, weights="f16")
+    assert gm.weights == "f16"
+    mel = mels(2, first=3)
+    enc = gm.encode(torch.from_numpy(mel).cuda()).cpu().numpy()
+    want = ref.encode(mel)
+    assert np.max(np.abs(enc - want)) <= 2e-3 * np.max(np.abs(want))
+    got = gm.transcribe(torch.from_numpy(mel).cuda(), 50259, max_tokens=16)
+    assert got == ref.transcribe(mel, 50259, max_tokens=16)
+    gm.close()
+
+
+def test_f16_gguf_checkpoint(torch, tmp_path):
+    import whisper_amd
+    import write_gguf
+
+    p = tmp_path / "f16.gguf"
+    write_gguf.write_synthetic_gguf(str(p), "tiny_test", SEED, linear="f16")
+    g = whisper_amd.WhisperModel.from_gguf(str(p), "tiny_test", max_batch=2)
+    s = whisper_amd.WhisperModel("tiny_test", SEED, max_batch=2, weights="f16")
+    assert g.weights == "f16"
+    mel = torch.from_numpy(mels(2, first=9)).cuda()
+    assert torch.equal(g.encode(mel), s.encode(mel))

@@ -380,3 +380,33 @@ def test_gemm_headmajor_layout(torch, policy):
     with pytest.raises(wq4.WQ4Error):
         wq4.check(L.wq4_gemm_tiled_headmajor(t.handle, None, ctypes.c_void_p(at.data_ptr()),
                                              ctypes.c_void_p(hm.data_ptr()), m, 25, d, wq4.PREC_F16X2, policy, st))
+
+
+# ------------------------------------------- f16 weights (BASELINE config 5) --
+@pytest.mark.parametrize("policy", [1, 2])
+@pytest.mark.parametrize("m,n,k", [(1, 1280, 1280), (32, 5120, 1280), (100, 1280, 5120), (1500, 1280, 1280),
+                                   (5, 96, 160)])
+def test_f16_weights_gemm(torch, policy, m, n, k):
+    """The same kernels on f16 weight fragments: x = hi + lo against the exact
+    f16 w, f32 accumulation -> the f16x2 tolerance of the Q4 path."""
+    rng = np.random.default_rng(41 + m + n)
+    w = (rng.standard_normal((n, k)) * 0.03).astype(np.float16)
+    t = wq4.Q4Tensor.from_f16(w)
+    assert t.weight_type == "f16"
+    assert np.array_equal(t.raw_bytes().view(np.float16).reshape(n, k), w)
+    assert np.array_equal(t.dequantize_host(), w.astype(np.float32))
+    x = rng.standard_normal(m * k).astype(np.float32)
+    wq4.set_kernel_policy(policy)
+    y = wq4.q4_matmul(to_dev(torch, x, (1, m, k)), t).cpu().numpy().reshape(m, n)
+    assert_q4_close(y, x.reshape(m, k), w.astype(np.float32), what="f16 weights")
+
+
+def test_f16_weights_batch_invariance(torch):
+    n, k = 1280, 1280
+    rng = np.random.default_rng(43)
+    t = wq4.Q4Tensor.from_f16((rng.standard_normal((n, k)) * 0.03).astype(np.float16))
+    wq4.set_kernel_policy(2)
+    xb = to_dev(torch, rng.standard_normal(32 * k).astype(np.float32), (32, 1, k))
+    yb = wq4.q4_matmul(xb, t).cpu().numpy()
+    y1 = wq4.q4_matmul(xb[5:6].contiguous(), t).cpu().numpy()
+    assert np.array_equal(yb[5:6].view(np.uint32), y1.view(np.uint32))

@@ -190,6 +190,7 @@ struct wa_model {
   // decode groups: the clips of a transcribe split over up to kMaxGroups
   // independent streams, each replaying its own step graph (see DecGroup)
   std::vector<DecGroup> groups;
+  int wtype = 0;     // linear weights: 0 Q4_0, 1 f16 (BASELINE config 5)
   int kv_batch = 0;  // clips of the last cross-K/V pass (V half offset of the head-major cache)
   hipStream_t own_stream = nullptr;  // encoder / cross-K/V (graph capture needs a non-null stream)
   float timings[5] = {0, 0, 0, 0, 0};
@@ -243,6 +244,8 @@ struct Source {
   virtual bool f32(const std::string& name, int64_t n, float lo, float hi, bool optional, std::vector<float>& out) = 0;
   // raw Q4_0 bytes of the [rows, k] weight `name` written at dst
   virtual bool q4(const std::string& name, int rows, int k, uint8_t* dst) = 0;
+  // f16 halves of the [rows, k] weight `name` written at dst (config 5)
+  virtual bool f16(const std::string& name, int rows, int k, uint16_t* dst) = 0;
   std::string err;
 };
 
@@ -263,6 +266,12 @@ struct SynthSource : Source {
     parallel_for(nblk, [&](int64_t a, int64_t b) {
       (void)wq4_quantize_q4_0(w.data() + a * 32, (b - a) * 32, dst + a * 18);
     });
+    return true;
+  }
+  bool f16(const std::string& name, int rows, int k, uint16_t* dst) override {
+    std::vector<float> w((size_t)rows * k);
+    synth_uniform(seed, name, (int64_t)rows * k, -lin_scale(k), lin_scale(k), w.data());
+    for (size_t i = 0; i < w.size(); ++i) dst[i] = __builtin_bit_cast(uint16_t, (_Float16)w[i]);
     return true;
   }
 };
@@ -311,6 +320,21 @@ struct GgufSource : Source {
     std::memcpy(dst, p, t->nbytes());
     return true;
   }
+  // config 5: F16 linear weights (the reference loader rejects them)
+  bool f16(const std::string& name, int rows, int k, uint16_t* dst) override {
+    const wa::GgufTensor* t = g.find(name);
+    if (!t) return bad("Tensor '" + name + "' not found");
+    if (t->type != wa::kGgmlF16)
+      return bad("Expected F16 for weight '" + name + "' (an F16 checkpoint), got " +
+                 (t->type == wa::kGgmlF32 ? "F32" : "Q4_0"));
+    if (t->dims.size() != 2 || t->dims[0] != (uint64_t)k || t->dims[1] != (uint64_t)rows)
+      return bad("F16 weight '" + name + "' has the wrong shape (expected [" + std::to_string(rows) + ", " +
+                 std::to_string(k) + "])");
+    const uint8_t* p = g.data(*t);
+    if (!p) return bad("Tensor '" + name + "' data lies outside the file");
+    std::memcpy(dst, p, t->nbytes());
+    return true;
+  }
 };
 
 struct Builder {
@@ -334,11 +358,28 @@ struct Builder {
     return v;
   }
   float* vec(const std::string& name, int64_t n, float lo, float hi) { return upload(get(name, n, lo, hi)); }
-  // Q4 weights of several GGUF tensors [n_i, k], row-concatenated (a fused projection).
+  // Linear weights of several GGUF tensors [n_i, k], row-concatenated (a
+  // fused projection): Q4_0 blocks, or f16 halves for an F16 model.
   wq4_tensor* q4(const std::vector<std::string>& names, const std::vector<int>& rows, int k) {
     if (st != WQ4_OK) return nullptr;
     int64_t total = 0;
     for (int r : rows) total += r;
+    if (m->wtype == 1) {
+      std::vector<uint16_t> h((size_t)(total * k));
+      size_t off = 0;
+      for (size_t i = 0; i < names.size(); ++i) {
+        if (!src.f16(names[i], rows[i], k, h.data() + off)) {
+          st = fail(WQ4_EINVAL, src.err);
+          return nullptr;
+        }
+        off += (size_t)rows[i] * k;
+      }
+      wq4_tensor* t = nullptr;
+      wq4_status s = wq4_tensor_create_f16(m->device, h.data(), total, k, &t);
+      if (s != WQ4_OK) st = fail(s, std::string("F16 weight upload: ") + wq4_last_error());
+      m->bytes += wq4_tensor_device_bytes(t);
+      return t;
+    }
     std::vector<uint8_t> raw((size_t)(total * k / 32 * 18));
     size_t off = 0;
     for (size_t i = 0; i < names.size(); ++i) {
@@ -755,13 +796,14 @@ wq4_status wa_synth_uniform(uint64_t seed, const char* name, int64_t n, float lo
   return WQ4_OK;
 }
 
-wq4_status wa_model_create_synthetic(int device, int variant, uint64_t seed, int max_batch, wq4_precision prec,
-                                     wa_model** out) {
+wq4_status wa_model_create_synthetic_ex(int device, int variant, uint64_t seed, int max_batch, wq4_precision prec,
+                                        int weight_type, wa_model** out) {
   if (!out) return fail(WQ4_EINVAL, "out is null");
   *out = nullptr;
   if (variant < 0 || variant > 2) return fail(WQ4_EINVAL, "unknown variant");
   if (max_batch < 1 || max_batch > 256) return fail(WQ4_EINVAL, "max_batch must be in [1, 256]");
   if (prec != WQ4_PREC_F16X2 && prec != WQ4_PREC_F16) return fail(WQ4_EINVAL, "unknown precision");
+  if (weight_type != 0 && weight_type != 1) return fail(WQ4_EINVAL, "weight_type must be 0 (Q4_0) or 1 (F16)");
   WA_HIP(hipSetDevice(device));
   std::unique_ptr<wa_model> m(new wa_model());
   m->device = device;
@@ -769,6 +811,7 @@ wq4_status wa_model_create_synthetic(int device, int variant, uint64_t seed, int
   m->prec = prec;
   m->ns = prec == WQ4_PREC_F16 ? 1 : 2;
   m->bmax = max_batch;
+  m->wtype = weight_type;
   SynthSource src(seed);
   wq4_status s = build_model(m.get(), src);
   if (s != WQ4_OK) return s;
@@ -778,6 +821,11 @@ wq4_status wa_model_create_synthetic(int device, int variant, uint64_t seed, int
   WA_HIP(hipDeviceSynchronize());
   *out = m.release();
   return WQ4_OK;
+}
+
+wq4_status wa_model_create_synthetic(int device, int variant, uint64_t seed, int max_batch, wq4_precision prec,
+                                     wa_model** out) {
+  return wa_model_create_synthetic_ex(device, variant, seed, max_batch, prec, 0, out);
 }
 
 wq4_status wa_model_create_from_gguf(int device, const char* path, int variant, int max_batch, wq4_precision prec,
@@ -796,6 +844,8 @@ wq4_status wa_model_create_from_gguf(int device, const char* path, int variant, 
   m->prec = prec;
   m->ns = prec == WQ4_PREC_F16 ? 1 : 2;
   m->bmax = max_batch;
+  const wa::GgufTensor* probe = file.find("encoder.blocks.0.attn.query.weight");
+  m->wtype = probe && probe->type == wa::kGgmlF16 ? 1 : 0;  // an F16 checkpoint (config 5)
   GgufSource src(file);
   wq4_status s = build_model(m.get(), src);
   if (s != WQ4_OK) return s;
@@ -861,6 +911,8 @@ wq4_status wa_gguf_tensor_data(const wa_gguf* g, const char* name, uint8_t* out,
   std::memcpy(out, p, t->nbytes());
   return WQ4_OK;
 }
+
+int wa_model_weight_type(const wa_model* m) { return m ? m->wtype : -1; }
 
 wq4_status wa_model_config(const wa_model* m, int32_t* cfg) {
   if (!m || !cfg) return fail(WQ4_EINVAL, "null argument");

@@ -33,6 +33,7 @@ struct wq4_tensor {
   float* cs = nullptr;       // device, g.colscale_bytes()
   uint8_t* raw = nullptr;    // device, raw GGUF bytes (flat tensors only)
   size_t raw_bytes = 0;
+  int wtype = 0;             // wq4::kWeightsQ4, or kWeightsF16 (nib = f16 fragments, sc unused, cs = 1)
 };
 
 namespace {
@@ -167,7 +168,7 @@ wq4_status gemm(const wq4_tensor* w, const _Float16* at, int64_t rows, const wq4
     wq4_status s = decode_ws_get(w->device, st, &ws);
     if (s != WQ4_OK) return s;
   }
-  hipError_t he = wq4::launch_q4_gemm(w->g, w->nib, w->sc, w->cs, at, (int)rows, e, mode, ns, ws, st);
+  hipError_t he = wq4::launch_q4_gemm(w->g, w->nib, w->sc, w->cs, at, (int)rows, e, mode, ns, ws, st, w->wtype);
   if (he != hipSuccess) return hip_fail(he, "q4_gemm launch");
   return WQ4_OK;
 }
@@ -276,12 +277,51 @@ int64_t wq4_tensor_num_blocks(const wq4_tensor* t) { return t ? t->g.n * t->g.k 
 int wq4_tensor_device(const wq4_tensor* t) { return t ? t->device : -1; }
 size_t wq4_tensor_device_bytes(const wq4_tensor* t) {
   if (!t) return 0;
+  if (t->wtype == wq4::kWeightsF16) return t->g.f16_frag_bytes() + t->g.colscale_bytes();
   return t->flat ? t->raw_bytes : t->g.nib_bytes() + t->g.sc_bytes() + t->g.colscale_bytes();
 }
+
+wq4_status wq4_tensor_create_f16(int device, const uint16_t* w, int64_t n, int64_t k, wq4_tensor** out) {
+  if (!out) return fail(WQ4_EINVAL, "out is null");
+  *out = nullptr;
+  if (n <= 0 || k <= 0 || k % 32 != 0)
+    return fail(WQ4_ESHAPE, "F16 weights need n > 0 and k % 32 == 0, got [" + std::to_string(n) + ", " +
+                                std::to_string(k) + "]");
+  if (n > (1 << 24) || k > (1 << 24)) return fail(WQ4_ESHAPE, "dimension too large for this build (> 2^24)");
+  if (!w) return fail(WQ4_EINVAL, "weights are null");
+  DeviceGuard dg(device);
+  if (!dg.ok) return fail(WQ4_EHIP, "hipSetDevice(" + std::to_string(device) + ") failed");
+  auto* t = new wq4_tensor();
+  t->device = device;
+  t->g = wq4::make_geom(n, k);
+  t->wtype = wq4::kWeightsF16;
+  std::vector<uint16_t> frag(t->g.f16_frag_bytes() / 2);
+  wq4::repack_f16(w, t->g, frag.data());
+  std::vector<float> ones(t->g.np, 1.0f);
+  hipError_t e = hipMalloc(&t->nib, t->g.f16_frag_bytes());
+  if (e == hipSuccess) e = hipMalloc(&t->cs, t->g.colscale_bytes());
+  if (e == hipSuccess) e = hipMemcpy(t->nib, frag.data(), t->g.f16_frag_bytes(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(t->cs, ones.data(), t->g.colscale_bytes(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    wq4_tensor_destroy(t);
+    return hip_fail(e, "F16 weight upload");
+  }
+  *out = t;
+  return WQ4_OK;
+}
+
+int wq4_tensor_weight_type(const wq4_tensor* t) { return t ? t->wtype : -1; }
 
 wq4_status wq4_tensor_raw_bytes(const wq4_tensor* t, uint8_t* host_out) {
   if (!t || !host_out) return fail(WQ4_EINVAL, "null argument");
   DeviceGuard dg(t->device);
+  if (t->wtype == wq4::kWeightsF16) {  // the f16 [N, K] halves as given
+    std::vector<uint16_t> frag(t->g.f16_frag_bytes() / 2);
+    hipError_t e = hipMemcpy(frag.data(), t->nib, t->g.f16_frag_bytes(), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "F16 weight read-back");
+    wq4::unrepack_f16(frag.data(), t->g, reinterpret_cast<uint16_t*>(host_out));
+    return WQ4_OK;
+  }
   if (t->flat) {
     hipError_t e = hipMemcpy(host_out, t->raw, t->raw_bytes, hipMemcpyDeviceToHost);
     return e == hipSuccess ? WQ4_OK : hip_fail(e, "Q4Tensor read-back");
@@ -302,6 +342,13 @@ static float f16_to_f32_host(uint16_t h) { return (float)__builtin_bit_cast(_Flo
 // Q4Tensor::dequantize, src/gguf/tensor.rs:88-113 (D2H, then host dequant).
 wq4_status wq4_tensor_dequantize(const wq4_tensor* t, float* host_out) {
   if (!t || !host_out) return fail(WQ4_EINVAL, "null argument");
+  if (t->wtype == wq4::kWeightsF16) {
+    std::vector<uint16_t> h((size_t)(t->g.n * t->g.k));
+    wq4_status s = wq4_tensor_raw_bytes(t, reinterpret_cast<uint8_t*>(h.data()));
+    if (s != WQ4_OK) return s;
+    for (size_t i = 0; i < h.size(); ++i) host_out[i] = f16_to_f32_host(h[i]);
+    return WQ4_OK;
+  }
   const int64_t nb = t->g.n * t->g.k / 32;
   std::vector<uint8_t> raw((size_t)nb * 18);
   wq4_status s = wq4_tensor_raw_bytes(t, raw.data());

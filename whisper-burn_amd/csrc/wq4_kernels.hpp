@@ -38,8 +38,11 @@ DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal);
 // y = epi((A W^T) * colscale).  epi_mode: 0 = f32 row-major, 1 = A-tiled f16
 // operand of a following GEMM.  ws != null selects the split-K decode kernel
 // (rows <= 128; larger row counts or unsupported shapes use the tile kernel).
+// wtype: kWeightsQ4 (nib/sc/colscale of wq4_layout.hpp) or kWeightsF16
+// (nib = repack_f16 fragments, sc unused, colscale = 1).
+constexpr int kWeightsQ4 = 0, kWeightsF16 = 1;
 hipError_t launch_q4_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* colscale,
                           const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int ns, const DecodeWs* ws,
-                          hipStream_t st);
+                          hipStream_t st, int wtype);
 
 }  // namespace wq4

@@ -104,4 +104,22 @@ void unrepack_q4(const uint8_t* nib, const uint32_t* sc, const float* colscale, 
   }
 }
 
+static inline size_t f16_frag_index(const Q4Geom& g, int64_t n, int64_t k) {
+  const int64_t nt = n / 32, r = n % 32, bp = k / 64, kb = k % 64;
+  const int64_t blk = kb / 32, kk = (kb / 16) % 2, h = (kb / 8) % 2, j = kb % 8;
+  const int64_t lane = r + 32 * h;
+  return (size_t)(((nt * g.nbp + bp) * 64 + lane) * 32 + (blk * 2 + kk) * 8 + j);
+}
+
+void repack_f16(const uint16_t* w, const Q4Geom& g, uint16_t* frag) {
+  std::memset(frag, 0, g.f16_frag_bytes());
+  for (int64_t n = 0; n < g.n; ++n)
+    for (int64_t k = 0; k < g.k; ++k) frag[f16_frag_index(g, n, k)] = w[n * g.k + k];
+}
+
+void unrepack_f16(const uint16_t* frag, const Q4Geom& g, uint16_t* w) {
+  for (int64_t n = 0; n < g.n; ++n)
+    for (int64_t k = 0; k < g.k; ++k) w[n * g.k + k] = frag[f16_frag_index(g, n, k)];
+}
+
 }  // namespace wq4

@@ -58,6 +58,7 @@ struct Q4Geom {
   size_t nib_bytes() const { return (size_t)ntiles * nbp * 1024; }
   size_t sc_bytes() const { return (size_t)ntiles * nbp * 32 * 4; }
   size_t colscale_bytes() const { return (size_t)np * 4; }
+  size_t f16_frag_bytes() const { return (size_t)ntiles * nbp * 4096; }  // F16 weights
 };
 
 inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
@@ -84,5 +85,13 @@ inline size_t atiled_bytes(int64_t rows, int64_t k, int ns) {
 void repack_q4(const uint8_t* raw, const Q4Geom& g, uint8_t* nib, uint32_t* sc, float* colscale);
 // Exact inverse (for Q4Tensor::dequantize and the lossless check).
 void unrepack_q4(const uint8_t* nib, const uint32_t* sc, const float* colscale, const Q4Geom& g, uint8_t* raw);
+
+// Unquantized f16 weights (BASELINE config 5; GGUF F16 linear tensors):
+// row-major [N, K] IEEE halves repacked into the same MFMA B-fragment order,
+//   frag[nt][bp][lane][blk][kk][8 halves]  (4 KiB per (nt, bp), 64 B a lane)
+//   lane l: n = 32 nt + (l & 31), k = 64 bp + 32 blk + 16 kk + 8 (l >> 5) + j
+// (zero beyond N / K): the kernels feed these halves to the MFMA as they are.
+void repack_f16(const uint16_t* w, const Q4Geom& g, uint16_t* frag);
+void unrepack_f16(const uint16_t* frag, const Q4Geom& g, uint16_t* w);
 
 }  // namespace wq4

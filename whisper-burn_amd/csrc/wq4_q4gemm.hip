@@ -132,7 +132,7 @@ __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >
 constexpr int kPrefillTM = 4;  // m-tiles (32 rows) per workgroup
 constexpr int kPrefillTN = 2;  // n-tiles (32 cols) per wave; 4 waves
 
-template <int NS, int EPI>
+template <int NS, int EPI, int WK>
 __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* __restrict__ nib,
                                                                  const uint32_t* __restrict__ sc,
                                                                  const float* __restrict__ colscale,
@@ -169,14 +169,23 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
     }
   };
 
-  u32x4 braw[TN];
+  // B: Q4 -> 16 B nibbles + a scale word per (n-tile, bp); F16 weights ->
+  // four 16 B fragments (blk, kk) per (n-tile, bp), used as they are
+  constexpr int BW = WK == kWeightsF16 ? 4 : 1;
+  u32x4 braw[TN][BW];
   uint32_t bsc[TN];
-  auto load_b = [&](int bp, u32x4* br, uint32_t* bs) {
+  auto load_b = [&](int bp, u32x4 (*br)[BW], uint32_t* bs) {
 #pragma unroll
     for (int nt = 0; nt < TN; ++nt) {
       const size_t t = (size_t)(nt0 + nt) * nbp + bp;
-      br[nt] = *reinterpret_cast<const u32x4*>(nib + (t * 64 + lane) * 16);
-      bs[nt] = sc[t * 32 + r];
+      if constexpr (WK == kWeightsF16) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) br[nt][q] = *reinterpret_cast<const u32x4*>(nib + (t * 64 + lane) * 64 + q * 16);
+        bs[nt] = 0;
+      } else {
+        br[nt][0] = *reinterpret_cast<const u32x4*>(nib + (t * 64 + lane) * 16);
+        bs[nt] = sc[t * 32 + r];
+      }
     }
   };
 
@@ -194,7 +203,7 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
 
   for (int bp = 0; bp < nbp; ++bp) {
     const bool more = bp + 1 < nbp;
-    u32x4 braw_n[TN];
+    u32x4 braw_n[TN][BW];
     uint32_t bsc_n[TN];
     if (more) {
       issue_a(bp + 1, (bp + 1) & 1);
@@ -207,9 +216,15 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
         half8 bh[TN][2], bl[TN][2];
 #pragma unroll
         for (int nt = 0; nt < TN; ++nt) {
-          const uint32_t dbits = blk ? (bsc[nt] >> 16) : (bsc[nt] & 0xffffu);
+          if constexpr (WK == kWeightsF16) {
 #pragma unroll
-          for (int kk = 0; kk < 2; ++kk) deq_scaled<NS>(braw[nt][blk * 2 + kk], dbits, bh[nt][kk], bl[nt][kk]);
+            for (int kk = 0; kk < 2; ++kk) bh[nt][kk] = __builtin_bit_cast(half8, braw[nt][blk * 2 + kk]);
+          } else {
+            const uint32_t dbits = blk ? (bsc[nt] >> 16) : (bsc[nt] & 0xffffu);
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+              deq_scaled<NS>(braw[nt][0][blk * 2 + kk], dbits, bh[nt][kk], bl[nt][kk]);
+          }
         }
 #pragma unroll
         for (int mt = 0; mt < TM; ++mt) {
@@ -224,7 +239,7 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
               acc[mt][nt] = mfma32(ahi, bh[nt][kk], acc[mt][nt]);
               if constexpr (NS == 2) {
                 acc[mt][nt] = mfma32(alo, bh[nt][kk], acc[mt][nt]);
-                acc[mt][nt] = mfma32(ahi, bl[nt][kk], acc[mt][nt]);
+                if constexpr (WK != kWeightsF16) acc[mt][nt] = mfma32(ahi, bl[nt][kk], acc[mt][nt]);
               }
             }
           }
@@ -234,7 +249,8 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
     if (more) {
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt) {
-        braw[nt] = braw_n[nt];
+#pragma unroll
+        for (int q = 0; q < BW; ++q) braw[nt][q] = braw_n[nt][q];
         bsc[nt] = bsc_n[nt];
       }
     }
@@ -374,7 +390,7 @@ __device__ __forceinline__ void decode_epilogue(const floatx16& s, float cs, int
   }
 }
 
-template <int NS, int EPI, int PER, int MT, int W>
+template <int NS, int EPI, int PER, int MT, int W, int WK>
 __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* __restrict__ nib,
                                                               const uint32_t* __restrict__ sc,
                                                               const float* __restrict__ colscale,
@@ -398,14 +414,24 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
 
   // this wave's weights (once-read stream: nt) -- zeros past cnt
   const size_t t0 = (size_t)nt * nbp + bp0;
-  const __amdgpu_buffer_rsrc_t rw = brsrc(nib + t0 * 1024, (uint32_t)cnt * 1024);
-  const __amdgpu_buffer_rsrc_t rsc = brsrc(sc + t0 * 32, (uint32_t)cnt * 128);
-  u32x4 br[PER];
+  constexpr int BW = WK == kWeightsF16 ? 4 : 1;  // 16 B weight loads per lane per bp
+  const __amdgpu_buffer_rsrc_t rw = brsrc(nib + t0 * 1024 * BW, (uint32_t)cnt * 1024 * BW);
+  u32x4 br[PER][BW];
   uint32_t bs[PER];
+  if constexpr (WK == kWeightsF16) {
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    br[i] = __builtin_amdgcn_raw_buffer_load_b128(rw, (i * 64 + lane) * 16, 0, 2);
-    bs[i] = __builtin_amdgcn_raw_buffer_load_b32(rsc, (i * 32 + r) * 4, 0, 2);
+    for (int i = 0; i < PER; ++i) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) br[i][q] = __builtin_amdgcn_raw_buffer_load_b128(rw, (i * 64 + lane) * 64 + q * 16, 0, 2);
+      bs[i] = 0;
+    }
+  } else {
+    const __amdgpu_buffer_rsrc_t rsc = brsrc(sc + t0 * 32, (uint32_t)cnt * 128);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      br[i][0] = __builtin_amdgcn_raw_buffer_load_b128(rw, (i * 64 + lane) * 16, 0, 2);
+      bs[i] = __builtin_amdgcn_raw_buffer_load_b32(rsc, (i * 32 + r) * 4, 0, 2);
+    }
   }
   // activation fragments of every m-tile, rows >= M read as zeros
   const size_t slab = (size_t)nbp * 2 * 2 * NS * 1024;  // bytes of one m-tile (kbp = 2 nbp)
@@ -441,17 +467,24 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
       if (i < cnt) {
 #pragma unroll
         for (int blk = 0; blk < 2; ++blk) {
-          const uint32_t dbits = blk ? (bs[i] >> 16) : (bs[i] & 0xffffu);
           half8 bh0, bl0, bh1, bl1;
-          deq_scaled<NS>(br[i][blk * 2 + 0], dbits, bh0, bl0);
-          deq_scaled<NS>(br[i][blk * 2 + 1], dbits, bh1, bl1);
+          if constexpr (WK == kWeightsF16) {
+            bh0 = __builtin_bit_cast(half8, br[i][blk * 2 + 0]);
+            bh1 = __builtin_bit_cast(half8, br[i][blk * 2 + 1]);
+          } else {
+            const uint32_t dbits = blk ? (bs[i] >> 16) : (bs[i] & 0xffffu);
+            deq_scaled<NS>(br[i][0][blk * 2 + 0], dbits, bh0, bl0);
+            deq_scaled<NS>(br[i][0][blk * 2 + 1], dbits, bh1, bl1);
+          }
           acc0 = mfma32(a[mt][i][blk][0][0], bh0, acc0);
           acc1 = mfma32(a[mt][i][blk][1][0], bh1, acc1);
           if constexpr (NS == 2) {
             acc0 = mfma32(a[mt][i][blk][0][1], bh0, acc0);
             acc1 = mfma32(a[mt][i][blk][1][1], bh1, acc1);
-            acc0 = mfma32(a[mt][i][blk][0][0], bl0, acc0);
-            acc1 = mfma32(a[mt][i][blk][1][0], bl1, acc1);
+            if constexpr (WK != kWeightsF16) {
+              acc0 = mfma32(a[mt][i][blk][0][0], bl0, acc0);
+              acc1 = mfma32(a[mt][i][blk][1][0], bl1, acc1);
+            }
           }
         }
       }
@@ -689,7 +722,7 @@ hipError_t launch_tile_activations(const float* x, _Float16* at, int M, int K, i
   return hipGetLastError();
 }
 
-template <int NS, int EPI>
+template <int NS, int EPI, int WK>
 static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* cs,
                                 const _Float16* at, int rows, const EpiArgs& e, const DecodeWs* ws,
                                 hipStream_t st) {
@@ -700,7 +733,7 @@ static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint3
   if (dec_ok) {
     const dim3 grid((unsigned)(g.ntiles * p.ks));
 #define WQ4_DEC(PER_, MT_, W_)                                                                               \
-  hipLaunchKernelGGL((q4_gemm_decode_kernel<NS, EPI, PER_, MT_, W_>), grid, dim3(64 * W_), decode_lds_bytes(W_), \
+  hipLaunchKernelGGL((q4_gemm_decode_kernel<NS, EPI, PER_, MT_, W_, WK>), grid, dim3(64 * W_), decode_lds_bytes(W_), \
                      st, nib, sc, cs, at, mt0, (int)g.nbp, p.ks, p.chunk, ws->part, ws->counters, e)
     // 8-wave plans: one m-tile per launch (two would not fit the registers);
     // 4-wave plans: m-tiles in launches of <= 2.  Launches on one stream
@@ -728,7 +761,7 @@ static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint3
   } else {
     const int ngroups = (int)((g.ntiles + 4 * kPrefillTN - 1) / (4 * kPrefillTN));
     const int mgroups = mtiles / kPrefillTM;
-    hipLaunchKernelGGL((q4_gemm_prefill_kernel<NS, EPI>), dim3((unsigned)(ngroups * mgroups)), dim3(256),
+    hipLaunchKernelGGL((q4_gemm_prefill_kernel<NS, EPI, WK>), dim3((unsigned)(ngroups * mgroups)), dim3(256),
                        prefill_lds_bytes(NS, EPI), st, nib, sc, cs, at, mtiles, (int)g.nbp, (int)g.ntiles, e);
   }
   return hipGetLastError();
@@ -736,15 +769,19 @@ static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint3
 
 hipError_t launch_q4_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* colscale,
                           const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int ns, const DecodeWs* ws,
-                          hipStream_t st) {
-#define WQ4_GEMM(NS_)                                                                                        \
+                          hipStream_t st, int wtype) {
+#define WQ4_GEMM(NS_, WK_)                                                                                   \
   switch (epi_mode) {                                                                                        \
-    case kEpiF32: return launch_gemm_t<NS_, kEpiF32>(g, nib, sc, colscale, at, rows, e, ws, st);             \
-    case kEpiTiled: return launch_gemm_t<NS_, kEpiTiled>(g, nib, sc, colscale, at, rows, e, ws, st);         \
-    default: return launch_gemm_t<NS_, kEpiHeadMajor>(g, nib, sc, colscale, at, rows, e, ws, st);            \
+    case kEpiF32: return launch_gemm_t<NS_, kEpiF32, WK_>(g, nib, sc, colscale, at, rows, e, ws, st);        \
+    case kEpiTiled: return launch_gemm_t<NS_, kEpiTiled, WK_>(g, nib, sc, colscale, at, rows, e, ws, st);    \
+    default: return launch_gemm_t<NS_, kEpiHeadMajor, WK_>(g, nib, sc, colscale, at, rows, e, ws, st);       \
   }
-  if (ns == 2) WQ4_GEMM(2);
-  WQ4_GEMM(1);
+  if (wtype == kWeightsF16) {
+    if (ns == 2) WQ4_GEMM(2, kWeightsF16);
+    WQ4_GEMM(1, kWeightsF16);
+  }
+  if (ns == 2) WQ4_GEMM(2, kWeightsQ4);
+  WQ4_GEMM(1, kWeightsQ4);
 #undef WQ4_GEMM
 }
 

@@ -57,9 +57,13 @@ def _align(off: int) -> int:
     return (off + ALIGNMENT - 1) // ALIGNMENT * ALIGNMENT
 
 
-def write_gguf(path: str, tensors: dict[str, np.ndarray], model_name: str, quantize=None) -> None:
+def write_gguf(path: str, tensors: dict[str, np.ndarray], model_name: str, quantize=None,
+               linear: str = "q4_0") -> None:
     """tensors: GGUF name -> f32 array (PyTorch shape).  quantize(array) ->
-    Q4_0 bytes (default: wq4.quantize_q4_0, the product quantizer)."""
+    Q4_0 bytes (default: wq4.quantize_q4_0, the product quantizer).
+    linear="f16" stores the tensors should_quantize() selects as F16 instead
+    (an unquantized checkpoint, BASELINE config 5 -- not something the
+    reference converter writes)."""
     if quantize is None:
         import wq4
 
@@ -67,7 +71,9 @@ def write_gguf(path: str, tensors: dict[str, np.ndarray], model_name: str, quant
     entries, blobs, cur = [], [], 0
     for name in sorted(tensors):
         a = np.asarray(tensors[name], np.float32)
-        if should_quantize(name, a.shape):
+        if should_quantize(name, a.shape) and linear == "f16":
+            data, dtype = a.astype(np.float16).tobytes(), GGML_F16
+        elif should_quantize(name, a.shape):
             data, dtype = bytes(quantize(a)), GGML_Q4_0
         else:
             data, dtype = a.astype(np.float32).tobytes(), GGML_F32
@@ -160,8 +166,8 @@ def synthetic_tensors(variant: str, seed: int) -> dict[str, np.ndarray]:
     return out
 
 
-def write_synthetic_gguf(path: str, variant: str, seed: int) -> None:
-    write_gguf(path, synthetic_tensors(variant, seed), f"synthetic-whisper-{variant}-seed{seed}")
+def write_synthetic_gguf(path: str, variant: str, seed: int, linear: str = "q4_0") -> None:
+    write_gguf(path, synthetic_tensors(variant, seed), f"synthetic-whisper-{variant}-seed{seed}", linear=linear)
 
 
 def main() -> None:
@@ -169,8 +175,9 @@ def main() -> None:
     ap.add_argument("--variant", default="tiny_test", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--linear", default="q4_0", choices=["q4_0", "f16"])
     a = ap.parse_args()
-    write_synthetic_gguf(a.out, a.variant, a.seed)
+    write_synthetic_gguf(a.out, a.variant, a.seed, a.linear)
     print(f"wrote {a.out} ({os.path.getsize(a.out) / 2**20:.1f} MiB)")
 
 

@@ -47,6 +47,10 @@ def lib() -> ctypes.CDLL:
         L.wa_profile_enable.argtypes = [vp, c_int]
         L.wa_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), c_int]
         L.wa_probe_kernels.argtypes = [vp, c_int, c_int, ctypes.POINTER(ctypes.c_double)]
+        L.wa_model_create_synthetic_ex.argtypes = [c_int, c_int, ctypes.c_uint64, c_int, c_int, c_int,
+                                                   ctypes.POINTER(vp)]
+        L.wa_model_weight_type.argtypes = [vp]
+        L.wa_model_weight_type.restype = c_int
         L.wa_model_create_from_gguf.argtypes = [c_int, ctypes.c_char_p, c_int, c_int, c_int, ctypes.POINTER(vp)]
         L.wa_gguf_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
         L.wa_gguf_close.argtypes = [vp]
@@ -61,7 +65,7 @@ def lib() -> ctypes.CDLL:
         L.wa_gguf_tensor_data.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t]
         for n in ("wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
                   "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read", "wa_probe_kernels",
-                  "wa_model_create_from_gguf", "wa_gguf_open", "wa_gguf_tensor_info", "wa_gguf_tensor_data"):
+                  "wa_model_create_from_gguf", "wa_model_create_synthetic_ex", "wa_gguf_open", "wa_gguf_tensor_info", "wa_gguf_tensor_data"):
             getattr(L, n).restype = c_int
         _lib = L
     return _lib
@@ -133,12 +137,14 @@ class WhisperModel:
     """A Whisper model resident on one MI355X: synthetic weights (default) or
     a GGUF checkpoint (WhisperModel.from_gguf, src/gguf/loader.rs)."""
 
+    WEIGHTS = {"q4_0": 0, "f16": 1}
+
     def __init__(self, variant: str = "large_v3", seed: int = 1234, max_batch: int = 1, device: int = 0,
-                 precision: int = wq4.PREC_F16X2, gguf_path: Optional[str] = None):
+                 precision: int = wq4.PREC_F16X2, gguf_path: Optional[str] = None, weights: str = "q4_0"):
         h = ctypes.c_void_p(None)
         if gguf_path is None:
-            check(lib().wa_model_create_synthetic(device, VARIANTS[variant], seed, max_batch, precision,
-                                                  ctypes.byref(h)))
+            check(lib().wa_model_create_synthetic_ex(device, VARIANTS[variant], seed, max_batch, precision,
+                                                     self.WEIGHTS[weights], ctypes.byref(h)))
         else:
             check(lib().wa_model_create_from_gguf(device, gguf_path.encode(), VARIANTS[variant], max_batch,
                                                   precision, ctypes.byref(h)))
@@ -149,6 +155,7 @@ class WhisperModel:
         cfg = (ctypes.c_int32 * len(CFG_KEYS))()
         check(lib().wa_model_config(h, cfg))
         self.config = dict(zip(CFG_KEYS, list(cfg)))
+        self.weights = {0: "q4_0", 1: "f16"}[lib().wa_model_weight_type(h)]
 
     @classmethod
     def from_gguf(cls, path: str, variant: str = "large_v3", max_batch: int = 1, device: int = 0,

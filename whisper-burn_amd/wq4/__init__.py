@@ -74,6 +74,9 @@ def _declare(L: ctypes.CDLL) -> None:
     L.wq4_ffn_forward_ws.argtypes = [vp, vp, vp, vp, vp, vp, vp, c_i64, ctypes.c_uint, c_int, vp, c_sz, vp]
     L.wq4_debug_repack.argtypes = [u8p, c_i64, c_i64, u8p, ctypes.POINTER(ctypes.c_uint32), f32p]
     L.wq4_quantize_q4_0.argtypes = [f32p, c_i64, u8p]
+    L.wq4_tensor_create_f16.argtypes = [c_int, ctypes.POINTER(ctypes.c_uint16), c_i64, c_i64, ctypes.POINTER(vp)]
+    L.wq4_tensor_weight_type.argtypes = [vp]
+    L.wq4_tensor_weight_type.restype = c_int
     L.wq4_debug_unrepack.argtypes = [u8p, ctypes.POINTER(ctypes.c_uint32), f32p, c_i64, c_i64, u8p]
     L.wq4_debug_repacked_bytes.argtypes = [c_i64, c_i64, ctypes.POINTER(c_sz), ctypes.POINTER(c_sz),
                                            ctypes.POINTER(c_sz)]
@@ -92,7 +95,7 @@ def _declare(L: ctypes.CDLL) -> None:
     for name in ("wq4_device_count", "wq4_set_precision", "wq4_set_kernel_policy", "wq4_tensor_create",
                  "wq4_tensor_shape", "wq4_tensor_dequantize", "wq4_tensor_raw_bytes", "wq4_matmul",
                  "wq4_linear_forward", "wq4_ffn_forward", "wq4_linear_forward_ws", "wq4_ffn_forward_ws",
-                 "wq4_debug_repack", "wq4_debug_unrepack", "wq4_debug_repacked_bytes", "wq4_quantize_q4_0"):
+                 "wq4_debug_repack", "wq4_debug_unrepack", "wq4_debug_repacked_bytes", "wq4_quantize_q4_0", "wq4_tensor_create_f16"):
         getattr(L, name).restype = c_int
 
 
@@ -214,6 +217,21 @@ class Q4Tensor:
         check(lib().wq4_tensor_create(device, _u8p(raw), raw.size, n, k, ctypes.byref(h)))
         return cls(h, (n, k), device)
 
+    @classmethod
+    def from_f16(cls, weights, device: int = 0) -> "Q4Tensor":
+        """Unquantized f16 weights [N, K] (BASELINE config 5): the same GEMM
+        entry points run on them (wq4_tensor_create_f16)."""
+        w = np.ascontiguousarray(np.asarray(weights), dtype=np.float16)
+        n, k = w.shape
+        h = ctypes.c_void_p(None)
+        check(lib().wq4_tensor_create_f16(device, w.view(np.uint16).ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)),
+                                          n, k, ctypes.byref(h)))
+        return cls(h, (n, k), device)
+
+    @property
+    def weight_type(self) -> str:
+        return {0: "q4_0", 1: "f16"}[lib().wq4_tensor_weight_type(self._h)]
+
     def shape(self) -> list[int]:
         """tensor.rs:74-76 -> [N, K]."""
         return [self._shape[0], self._shape[1]]
@@ -246,7 +264,7 @@ class Q4Tensor:
 
     def raw_bytes(self) -> np.ndarray:
         n, k = self._shape
-        out = np.empty(n * k // 32 * 18, np.uint8)
+        out = np.empty(n * k * 2 if self.weight_type == "f16" else n * k // 32 * 18, np.uint8)
         check(lib().wq4_tensor_raw_bytes(self._h, _u8p(out)))
         return out
 
