@@ -127,6 +127,9 @@ def main() -> None:
     ap.add_argument("--precision", default="f16x2", choices=["f16x2", "f16"])
     ap.add_argument("--weights", default="q4_0", choices=["q4_0", "f16"],
                     help="linear weights: Q4_0 (default) or unquantized f16 (BASELINE config 5)")
+    ap.add_argument("--audio", action="store_true",
+                    help="start from 16 kHz samples in HBM: the GPU log-mel front-end (wa_log_mel) runs inside "
+                         "the timed region")
     ap.add_argument("--fixed-length", action="store_true", help="ignore EOT (always max-tokens steps)")
     ap.add_argument("--cpu-rows", type=int, default=750)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -162,10 +165,38 @@ def main() -> None:
         arr = np.stack([whisper_amd.synth_uniform(0x5EED0000 + c, "mel", n_mels * 3000, -1.5, 1.0) for c in ids])
         return torch.from_numpy(arr.reshape(len(ids), n_mels, 3000)).to(f"cuda:{local_rank}")
 
-    mels = [batch(ids) for ids in clip_ids(rank, B, args.warmup, args.steps)]  # resident in HBM before timing
+    def audio_batch(ids: list[int]):
+        # speech-like synthetic audio: two per-clip tones under a 4 Hz envelope + noise, [B, 480000] f32
+        t = np.arange(480000, dtype=np.float64) / 16000.0
+        rows = []
+        for c in ids:
+            rng = np.random.default_rng(0x5EED0000 + c)
+            f1, f2 = 100.0 + 3.0 * (c % 97), 900.0 + 17.0 * (c % 89)
+            x = 0.3 * (0.5 + 0.5 * np.sin(2 * np.pi * 4.0 * t + c)) * np.sin(2 * np.pi * f1 * t)
+            x += 0.1 * np.sin(2 * np.pi * f2 * t) + 0.02 * rng.standard_normal(t.size)
+            rows.append(x.astype(np.float32))
+        return torch.from_numpy(np.stack(rows)).to(f"cuda:{local_rank}")
+
+    make = audio_batch if args.audio else batch
+    inputs = [make(ids) for ids in clip_ids(rank, B, args.warmup, args.steps)]  # resident in HBM before timing
+    mel_buf = torch.empty((B, n_mels, 3000), device=f"cuda:{local_rank}", dtype=torch.float32)
+    mel_ms = []
+
+    def run(x):
+        if not args.audio:
+            return model.transcribe(x, lang, args.max_tokens, eot_stop=not args.fixed_length)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        whisper_amd.log_mel(x, n_mels, out=mel_buf)
+        e1.record()
+        toks = model.transcribe(mel_buf, lang, args.max_tokens, eot_stop=not args.fixed_length)
+        mel_ms.append(e0.elapsed_time(e1))
+        return toks
+
     lang = None if args.lang < 0 else args.lang
     for s in range(args.warmup):
-        model.transcribe(mels[s], lang, args.max_tokens, eot_stop=not args.fixed_length)
+        run(inputs[s])
+    mel_ms.clear()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -175,7 +206,7 @@ def main() -> None:
     timings = []
     t0 = time.perf_counter()
     for s in range(args.steps):
-        toks = model.transcribe(mels[args.warmup + s], lang, args.max_tokens, eot_stop=not args.fixed_length)
+        toks = run(inputs[args.warmup + s])
         ntok += [len(t) for t in toks]
         timings.append(model.last_timings())
     torch.cuda.synchronize()
@@ -222,7 +253,7 @@ def main() -> None:
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp16x2" if prec == wq4.PREC_F16X2 else "fp16", "data": "synthetic",
             "config": {"workload": f"Whisper {args.variant} {args.weights.upper()}, {B} synthetic 30-s clips per GPU per step "
-                                   f"(BASELINE config 4 shard), greedy KV-cached decode, max {args.max_tokens} "
+                                   f"(BASELINE config 4 shard){', from audio' if args.audio else ''}, greedy KV-cached decode, max {args.max_tokens} "
                                    f"tokens, {'fixed length' if args.fixed_length else 'EOT stop'}",
                        "model": f"whisper-{args.variant.replace('_', '-')}-{args.weights} (synthetic weights)",
                        "global_batch": clips // args.steps, "seq_len": cfg["n_audio_ctx"],
@@ -239,6 +270,8 @@ def main() -> None:
             "phase_ms": {k: round(float(np.mean([t[k] for t in timings])), 3)
                          for k in ("encoder_ms", "cross_kv_ms", "prompt_ms", "decode_ms")},
             "decode_steps": [t["steps"] for t in timings],
+            "input": "16 kHz audio in HBM (GPU log-mel timed)" if args.audio else "log-mel in HBM",
+            "log_mel_ms": round(float(np.mean(mel_ms)), 3) if mel_ms else None,
             "model_load_s": round(t_load, 2),
         }
         if not args.no_cpu_baseline and world == 1:

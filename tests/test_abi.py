@@ -135,3 +135,16 @@ def test_precision_and_policy_setters():
     with pytest.raises(wq4.WQ4Error):
         wq4.set_kernel_policy(9)
     wq4.set_kernel_policy(0)
+
+
+def test_every_whisper_header_function_is_exported():
+    import re
+
+    import whisper_amd
+
+    text = re.sub(r"/\*.*?\*/", "", open(whisper_amd.HEADER_PATH).read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b(wa_[a-z0-9_]+)\s*\(", text)))
+    assert len(names) >= 20
+    L = whisper_amd.lib()
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing

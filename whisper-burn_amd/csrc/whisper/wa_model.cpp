@@ -22,7 +22,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -31,6 +33,7 @@
 #include "../../../include/wq4.h"
 #include "wa_gguf.hpp"
 #include "wa_kernels.hpp"
+#include "wa_mel.hpp"
 
 namespace {
 
@@ -1156,6 +1159,67 @@ wq4_status wa_probe_kernels(wa_model* m, int n_clips, int iters, double* out) {
   out[4] = 2.0 * B * F * D;
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
+  return WQ4_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- log-mel --
+// Per-device constants (window, filterbank, twiddles; per n_mels) and the
+// per-workgroup-max scratch, allocated on first use outside stream capture.
+namespace {
+struct MelDevice {
+  std::map<int, uint8_t*> consts;
+  float* part = nullptr;
+  int part_clips = 0;
+};
+std::mutex g_mel_mu;
+std::map<int, MelDevice> g_mel;
+}  // namespace
+
+extern "C" {
+
+wq4_status wa_log_mel(int device, const float* audio_dev, int n_clips, int64_t n_samples, int64_t ld_audio,
+                      int n_mels, float* mel_dev, void* stream) {
+  if (!mel_dev || (!audio_dev && n_samples > 0)) return fail(WQ4_EINVAL, "null argument");
+  if (n_clips < 1) return fail(WQ4_EINVAL, "n_clips must be >= 1");
+  if (n_samples < 0 || ld_audio < n_samples) return fail(WQ4_EINVAL, "need 0 <= n_samples <= ld_audio");
+  if (n_mels < 1 || n_mels > wa::kMelMaxMels) return fail(WQ4_EINVAL, "n_mels must be in [1, 256]");
+  WA_HIP(hipSetDevice(device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  std::lock_guard<std::mutex> lk(g_mel_mu);
+  MelDevice& md = g_mel[device];
+  uint8_t*& c = md.consts[n_mels];
+  if (!c || md.part_clips < n_clips) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    WA_HIP(hipStreamIsCapturing(st, &cs));
+    if (cs != hipStreamCaptureStatusNone)
+      return fail(WQ4_EINVAL, "wa_log_mel: run once outside stream capture first (allocates constants)");
+  }
+  if (!c) {
+    const wa::MelBank bank = wa::make_mel_bank(n_mels);
+    std::vector<uint8_t> host(wa::mel_const_bytes(n_mels));
+    wa::mel_pack_consts(bank, host.data());
+    WA_HIP(hipMalloc(reinterpret_cast<void**>(&c), host.size()));
+    WA_HIP(hipMemcpy(c, host.data(), host.size(), hipMemcpyHostToDevice));
+  }
+  if (md.part_clips < n_clips) {
+    WA_HIP(hipDeviceSynchronize());
+    if (md.part) WA_HIP(hipFree(md.part));
+    md.part = nullptr;
+    md.part_clips = 0;
+    WA_HIP(hipMalloc(reinterpret_cast<void**>(&md.part), (size_t)n_clips * wa::kMelWgPerClip * sizeof(float)));
+    md.part_clips = n_clips;
+  }
+  WA_HIP(wa::launch_log_mel(audio_dev, n_clips, n_samples, ld_audio, n_mels, c, md.part, mel_dev, st));
+  return WQ4_OK;
+}
+
+wq4_status wa_mel_filterbank(int n_mels, float* filters_out, float* window_out) {
+  if (n_mels < 1 || n_mels > wa::kMelMaxMels) return fail(WQ4_EINVAL, "n_mels must be in [1, 256]");
+  const wa::MelBank bank = wa::make_mel_bank(n_mels);
+  if (filters_out) std::memcpy(filters_out, bank.filters.data(), bank.filters.size() * sizeof(float));
+  if (window_out) std::memcpy(window_out, bank.window.data(), bank.window.size() * sizeof(float));
   return WQ4_OK;
 }
 

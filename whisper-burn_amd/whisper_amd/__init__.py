@@ -63,7 +63,9 @@ def lib() -> ctypes.CDLL:
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(c_int),
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.wa_gguf_tensor_data.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t]
-        for n in ("wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
+        L.wa_log_mel.argtypes = [c_int, vp, c_int, c_i64, c_i64, c_int, vp, vp]
+        L.wa_mel_filterbank.argtypes = [c_int, f32p, f32p]
+        for n in ("wa_log_mel", "wa_mel_filterbank", "wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
                   "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read", "wa_probe_kernels",
                   "wa_model_create_from_gguf", "wa_model_create_synthetic_ex", "wa_gguf_open", "wa_gguf_tensor_info", "wa_gguf_tensor_data"):
             getattr(L, n).restype = c_int
@@ -86,6 +88,40 @@ def _torch():
     import torch
 
     return torch
+
+
+MEL_FRAMES = 3000
+MEL_CHUNK = 480000
+
+
+def mel_filterbank(n_mels: int = 128) -> tuple[np.ndarray, np.ndarray]:
+    """(filters [n_mels, 201], periodic Hann window [400]) as the product builds
+    them (src/audio/mel.rs:272-320); host-only."""
+    fb = np.empty((n_mels, 201), np.float32)
+    win = np.empty(400, np.float32)
+    f32p = ctypes.POINTER(ctypes.c_float)
+    check(lib().wa_mel_filterbank(n_mels, fb.ctypes.data_as(f32p), win.ctypes.data_as(f32p)))
+    return fb, win
+
+
+def log_mel(audio, n_mels: int = 128, n_samples: Optional[int] = None, out=None):
+    """MelSpectrogram::compute_log (src/audio/mel.rs:126-157) with the pad /
+    truncate / transpose of transcribe.rs:44-76, for a batch of clips on the
+    GPU.  audio: cuda f32 [B, L] (16 kHz mono; the first n_samples of each row
+    are used, default L) -> cuda f32 [B, n_mels, 3000], the transcribe input."""
+    torch = _torch()
+    assert audio.dtype == torch.float32 and audio.is_cuda and audio.dim() == 2
+    if audio.stride(1) != 1:
+        audio = audio.contiguous()
+    B, L = audio.shape
+    n = L if n_samples is None else int(n_samples)
+    if out is None:
+        out = torch.empty((B, n_mels, MEL_FRAMES), device=audio.device, dtype=torch.float32)
+    dev = audio.device.index if audio.device.index is not None else torch.cuda.current_device()
+    check(lib().wa_log_mel(dev, ctypes.c_void_p(audio.data_ptr()), B, n, audio.stride(0), n_mels,
+                           ctypes.c_void_p(out.data_ptr()),
+                           ctypes.c_void_p(torch.cuda.current_stream(audio.device).cuda_stream)))
+    return out
 
 
 class GgufReader:
@@ -183,6 +219,13 @@ class WhisperModel:
                                   -1 if lang_token is None else int(lang_token), max_tokens, 1 if eot_stop else 0,
                                   toks.ctypes.data_as(i32p), nt.ctypes.data_as(i32p), self._stream()))
         return [toks[b, : nt[b]].tolist() for b in range(B)]
+
+    def transcribe_audio(self, audio, lang_token: Optional[int] = 50259, max_tokens: int = 224,
+                         eot_stop: bool = True, n_samples: Optional[int] = None):
+        """src/transcribe.rs:34-107 from 16 kHz samples (cuda f32 [B, L]) to
+        token ids: GPU log-mel (log_mel) then transcribe."""
+        mel = log_mel(audio, self.config["n_mels"], n_samples)
+        return self.transcribe(mel, lang_token, max_tokens, eot_stop)
 
     def last_timings(self) -> dict:
         t = (ctypes.c_float * 5)()
