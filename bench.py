@@ -6,7 +6,7 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 One "step" = one batch of synthetic 30-s clips transcribed end to end on each
-GPU: conv front-end + 32-layer encoder + cross-K/V + prompt + greedy KV-cached
+GPU: conv front-end + 32-layer encoder + prompt + greedy KV-cached
 decode (whisper.rs:51-128), mel already resident in HBM, token ids back on the
 host.  Workload at N = 1: BASELINE.json config 4's per-GPU shard (32 clips of
 the 256-clip / 8-GPU job); each rank runs its own clips (weak scaling, no
@@ -16,9 +16,10 @@ value = audio seconds of all ranks' clips / max-over-ranks wall seconds.
 roofline: the dominant kernel by time per step -- the Q4 GEMMs (north-star
 kernel, MFMA tile kernel, timed live with HIP events on their launch stream
 during the timed steps; algorithmic FLOPs = 2*M*N*K per launch) or the decode
-step's cross-attention (HBM stream of the cached K/V; HIP-event timed by
-wa_probe_kernels right after the timed steps; algorithmic bytes = K + V of
-every clip).  Both, and the decode-step fc1 GEMM, are reported.  cpu_baseline: the reference's CPU dequant->GEMM
+step's cross-attention (HBM stream of every clip's encoder output, f16 hi/lo
+planes, shared by all heads -- no per-layer K/V caches; HIP-event timed by
+wa_probe_kernels right after the timed steps; algorithmic bytes = encoder
+planes + raw Wk, Wv + operands).  Both, and the decode-step fc1 GEMM, are reported.  cpu_baseline: the reference's CPU dequant->GEMM
 path (src/gguf/tests.rs:60-87,172-184, restated in oracle/q4_oracle.c), one
 core, on one Large-V3 encoder layer's Q4 GEMMs at --cpu-rows rows, scaled to
 a clip's Q4 GEMM FLOPs (a lower bound on the CPU's per-clip time).
@@ -236,8 +237,9 @@ def main() -> None:
         xa = probe["cross_attention"]
         xa_gbs = xa["bytes"] / (xa["us"] * 1e-6) * 1e-9
         roof_xa = {"bound": "hbm", "achieved": round(xa_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                   "frac": round(xa_gbs / PEAK_HBM_GBS, 4), "traffic": pmc_traffic("cross_attn_kernel"),
-                   "kernel": "cross_attn_kernel (decode step, Tq = 1)", "avg_us": round(xa["us"], 2),
+                   "frac": round(xa_gbs / PEAK_HBM_GBS, 4), "traffic": pmc_traffic("xattn_main_kernel"),
+                   "kernel": "cross-attention over the encoder output: xattn_q + xattn_main + xattn_merge + "
+                             "xattn_out (decode step, Tq = 1)", "avg_us": round(xa["us"], 2),
                    "bytes_per_launch": xa["bytes"],
                    "total_ms_per_step": round(xa["us"] * 1e-3 * cfg["n_text_layer"] * steps_run, 2)}
         dq = probe["decode_fc1"]

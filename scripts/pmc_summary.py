@@ -14,7 +14,7 @@ import re
 import sys
 
 FAMILIES = {"q4_gemm_prefill_kernel": r"q4_gemm_prefill_kernel", "q4_gemm_decode_kernel": r"q4_gemm_decode_kernel",
-            "cross_attn_kernel": r"cross_attn_kernel<2, 1>|cross_attn_kernelILi2ELi1E"}
+            "xattn_main_kernel": r"xattn_main_kernel"}
 
 
 def load(counter: str, rnd: str) -> dict:

@@ -337,136 +337,6 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
   return hipGetLastError();
 }
 
-// ------------------------------------------------- cross-attention --
-// Memory-bound GEMV over the cross K/V cache (B * 1500 * 2D floats per
-// layer and step).  Grid = (H * S, B): the T encoder keys of each (head,
-// clip) are split over S workgroups (S depends on T only -> batch
-// invariant) so the chip sees ~10 balanced workgroups per CU instead of 2-3
-// unbalanced ones.  With S > 1 each workgroup publishes (m, l, o[64]) per
-// query write-through (sc1); the last arriver of the (head, clip) merges the
-// S partials in split order (cdna_hip_programming.md Guideline 16, R1) and
-// writes the A-tiled operand of the output projection.
-constexpr int kXattnMaxSplit = 8;
-constexpr int kXattnPart = 68;  // floats per (query) partial: o[64], m, l, pad
-
-int cross_attention_splits(int T) {
-  const int s = T / 375;
-  return s < 1 ? 1 : (s > kXattnMaxSplit ? kXattnMaxSplit : s);
-}
-
-template <int NS, int TQ>
-__global__ __launch_bounds__(256) void cross_attn_kernel(const float* __restrict__ q, const float* __restrict__ kc,
-                                                         const float* __restrict__ vc, int Tq_, int T, int H, int S,
-                                                         float* __restrict__ part,
-                                                         int* __restrict__ counters, _Float16* __restrict__ tiled) {
-  // TQ = 1 (decode step) keeps one query's state: ~half the VGPRs, twice the
-  // resident waves of the TQ = 4 (prompt) instance
-  const int Tq = TQ == 1 ? 1 : Tq_;
-  __shared__ float wm[4][TQ], wl[4][TQ];
-  __shared__ float wo[4][TQ][64];
-  __shared__ int last_flag;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int head = blockIdx.x / S, split = blockIdx.x - head * S, b = blockIdx.y;
-  const int D = H * 64;
-  const int sub = lane & 15, grp = lane >> 4;
-  floatx4 qv[TQ];
-#pragma unroll
-  for (int t = 0; t < TQ; ++t)
-    qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(q + (size_t)(b * Tq + t) * D + head * 64 + sub * 4) * 0.125f
-                   : floatx4{0.f, 0.f, 0.f, 0.f};
-  const int per_split = (T + S - 1) / S;
-  const int s0 = split * per_split, s1 = min(T, s0 + per_split);
-  const int per_wave = (s1 - s0 + 3) / 4;
-  const int k0 = min(s1, s0 + wave * per_wave), k1 = min(s1, k0 + per_wave);
-  // head-major K / V: [clip][head][T][64] each (wq4_gemm_tiled_headmajor)
-  const size_t hofs = ((size_t)b * H + head) * T * 64 + sub * 4;
-  const float* kb = kc + hofs;
-  const float* vb = vc + hofs;
-  float m[TQ], l[TQ];
-  floatx4 o[TQ];
-  attn_scan<TQ, 8>(
-      qv, Tq, k0, k1, grp,
-      [&](int j, const float*& kp, const float*& vp) {
-        kp = kb + (size_t)j * 64;
-        vp = vb + (size_t)j * 64;
-      },
-      [](int, int) { return true; }, m, l, o);
-  float mn, ls, os;
-  attn_merge<TQ>(Tq, wave, lane, m, l, o, wm, wl, wo, mn, ls, os);
-  if (S > 1) {
-    typedef __attribute__((address_space(1))) float gfloat;
-    typedef __attribute__((address_space(1))) int gint;
-    const size_t bh = (size_t)b * H + head;
-    if (wave < Tq) {  // publish this split's partial write-through
-      gfloat* pp = (gfloat*)(part + ((bh * S + split) * 4 + wave) * kXattnPart);
-      __hip_atomic_store(pp + lane, os, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (lane == 0) __hip_atomic_store(pp + 64, mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (lane == 1) __hip_atomic_store(pp + 65, ls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-    __syncthreads();
-    if (tid == 0) {
-      const int prev = __hip_atomic_fetch_add((gint*)(counters + bh), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last_flag = prev == S - 1;
-      if (prev == S - 1) __hip_atomic_store((gint*)(counters + bh), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!last_flag || wave >= Tq) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: loads stay below the ticket
-    // merge the S partials in split order (sc1 loads of sc1-stored bytes)
-    float pm[kXattnMaxSplit], pl[kXattnMaxSplit], po[kXattnMaxSplit];
-#pragma unroll
-    for (int sp = 0; sp < kXattnMaxSplit; ++sp) {
-      if (sp < S) {
-        gfloat* pp = (gfloat*)(part + ((bh * S + sp) * 4 + wave) * kXattnPart);
-        po[sp] = __hip_atomic_load(pp + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pm[sp] = __hip_atomic_load(pp + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pl[sp] = __hip_atomic_load(pp + 65, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    mn = -INFINITY;
-#pragma unroll
-    for (int sp = 0; sp < kXattnMaxSplit; ++sp)
-      if (sp < S) mn = fmaxf(mn, pm[sp]);
-    ls = 0.0f;
-    os = 0.0f;
-#pragma unroll
-    for (int sp = 0; sp < kXattnMaxSplit; ++sp) {
-      if (sp < S) {
-        const float a = pm[sp] == -INFINITY ? 0.0f : expf(pm[sp] - mn);
-        ls += pl[sp] * a;
-        os += po[sp] * a;
-      }
-    }
-  }
-  if (wave < Tq) {
-    const int t = wave;
-    const float val = os / ls;
-    const float v1 = __shfl_down(val, 1, 64), v2 = __shfl_down(val, 2, 64), v3 = __shfl_down(val, 3, 64);
-    if ((lane & 3) == 0) atile_store4<NS>(tiled, b * Tq + t, head * 64 + lane, kbp_of(D), val, v1, v2, v3);
-  }
-}
-
-hipError_t launch_cross_attention(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
-                                  float* part, int* counters, _Float16* tiled, int ns, hipStream_t st) {
-  if (Tq > 4) return hipErrorInvalidValue;
-  const int S = cross_attention_splits(T);
-  const dim3 grid(H * S, B), block(256);
-#define WA_XATTN(NS_, TQ_) \
-  hipLaunchKernelGGL((cross_attn_kernel<NS_, TQ_>), grid, block, 0, st, q, k, v, Tq, T, H, S, part, counters, tiled)
-  if (ns == 2) {
-    if (Tq == 1) WA_XATTN(2, 1); else WA_XATTN(2, 4);
-  } else {
-    if (Tq == 1) WA_XATTN(1, 1); else WA_XATTN(1, 4);
-  }
-#undef WA_XATTN
-  return hipGetLastError();
-}
-
-size_t cross_attention_part_floats(int B, int H, int T) {
-  return (size_t)B * H * cross_attention_splits(T) * 4 * kXattnPart;
-}
-
 // ------------------------------------------------------ conv + GELU --
 // out[b, t, n] = gelu(bias[n] + sum_{kk, c} in(b, c, t*S + kk - 1) W[n, c, kk])
 // (+ pos[t, n]).  GEMM view: rows (b, t), cols n, K = 3C (k = kk*C + c, the

@@ -30,15 +30,26 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
                                          int ctx, const DecodeState* state, int kv_len_host, _Float16* tiled,
                                          int ns, hipStream_t st);
 
-// Cross-attention over cached encoder K/V (attention.rs:161-236).  q: [B*Tq,
-// D] f32; kv: [B*T, 2D] f32 (k | v).  Writes the A-tiled operand.
-// Cross-attention over the cached encoder K / V (head-major [clip][head][T][64]
-// at k and v); part / counters: split-merge
-// workspace (cross_attention_part_floats floats, B * H zeroed ints).
-int cross_attention_splits(int T);
-size_t cross_attention_part_floats(int B, int H, int T);
-hipError_t launch_cross_attention(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
-                                  float* part, int* counters, _Float16* tiled, int ns, hipStream_t st);
+// Cross-attention over the encoder output (wa_xattn.hip; attention.rs:
+// 204-298 restated without K/V caches): q [B*Tq, D] f32 (rows b*Tq + i),
+// wk / wv: the layer's raw key / value weights [D, D] (wtype: Q4_0 blocks or
+// f16), bv: value bias, enc: [B][T][ns][D] f16 planes (launch_enc_planes),
+// qt: [B*Tq][ns][ceil16(H)][D] f16 scratch zeroed once, part:
+// xattn_part_floats floats.  Writes the A-tiled operand of the output
+// projection.  Needs D == 64 * H, D % 128 == 0, D <= 1280.
+struct XattnPlan {
+  int splits;  // frame ranges per query row (workgroups per row)
+  int ch;      // 16-frame sub-chunks per range
+};
+XattnPlan xattn_plan(int R, int T);
+size_t xattn_part_floats(int R, int H, int D, int T);
+hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, const float* bv, int wtype,
+                        const _Float16* enc, int B, int Tq, int T, int H, int D, _Float16* qt, float* part,
+                        _Float16* tiled, int ns, hipStream_t st);
+// A-tiled operand [R][K] (hi + lo) -> f32 rows (diagnostics).
+hipError_t launch_untile(const _Float16* tiled, int R, int K, int ns, float* out, hipStream_t st);
+// f32 rows [rows][D] -> [rows][ns][D] f16 planes (hi | lo) for launch_xattn.
+hipError_t launch_enc_planes(const float* x, int64_t rows, int D, int ns, _Float16* out, hipStream_t st);
 
 // Conv1D (layers.rs:77-132) as an implicit-im2col f32 MFMA GEMM + bias +
 // GELU (encoder.rs:89-94) (+ pos[t] if pos != nullptr).  Input element

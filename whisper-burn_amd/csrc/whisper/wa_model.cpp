@@ -144,10 +144,12 @@ struct EncLayer {
 };
 struct DecLayer {
   float *ln1_w, *ln1_b, *ln2_w, *ln2_b, *ln3_w, *ln3_b;
-  float *qkv_b, *out_b, *cq_b, *ckv_b, *cout_b, *fc1_b, *fc2_b;
-  wq4_tensor *qkv = nullptr, *out = nullptr, *cq = nullptr, *ckv = nullptr, *cout = nullptr, *fc1 = nullptr,
-             *fc2 = nullptr;
-  float *cache_k, *cache_v, *cross_kv;
+  float *qkv_b, *out_b, *cq_b, *cv_b, *cout_b, *fc1_b, *fc2_b;
+  wq4_tensor *qkv = nullptr, *out = nullptr, *cq = nullptr, *cout = nullptr, *fc1 = nullptr, *fc2 = nullptr;
+  // cross-attention key / value weights in raw GGUF form (Q4_0 blocks or
+  // f16), read by the K/V-cache-free cross-attention (wa_xattn.hip)
+  uint8_t *ck_raw = nullptr, *cv_raw = nullptr;
+  float *cache_k, *cache_v;
 };
 
 // One decode group: a contiguous range of clips [b0, b0 + nb) decoded on its
@@ -164,8 +166,8 @@ struct DecGroup {
   float *xd, *qkvd, *qd, *hid, *logits;
   _Float16 *atd_dec, *atf_dec;
   int *prompt_tok, *next_tok, *tokens, *ntok, *done;
-  float* xattn_part;    // cross-attention split partials
-  int* xattn_counters;  // per (clip, head) arrival tickets, re-armed in-kernel
+  _Float16* xqt;    // cross-attention Wk^T q operands [rows][ns][16*ceil(H/16)][D]
+  float* xattn_part;  // cross-attention split partials (Z, max, sum)
   wa::DecodeState* state;
   int* host_ndone = nullptr;  // pinned ring
   hipGraphExec_t graph = nullptr;
@@ -189,12 +191,16 @@ struct wa_model {
   std::vector<DecLayer> dec;
   // encoder activations
   float *h1, *x, *qkv;
-  _Float16 *at_d, *at_f, *enc_at;
+  _Float16 *at_d, *at_f;
+  // encoder output as f16 planes [clip][T][ns][D], the cross-attention's
+  // only per-clip state (no per-layer K/V caches)
+  _Float16* enc_planes = nullptr;
+  const float* enc_f32 = nullptr;  // ln_post output of the last encoder pass
   // decode groups: the clips of a transcribe split over up to kMaxGroups
   // independent streams, each replaying its own step graph (see DecGroup)
   std::vector<DecGroup> groups;
   int wtype = 0;     // linear weights: 0 Q4_0, 1 f16 (BASELINE config 5)
-  int kv_batch = 0;  // clips of the last cross-K/V pass (V half offset of the head-major cache)
+  int kv_batch = 0;  // clips of the last encoder pass (enc_planes valid for [0, kv_batch))
   hipStream_t own_stream = nullptr;  // encoder / cross-K/V (graph capture needs a non-null stream)
   float timings[5] = {0, 0, 0, 0, 0};
   // live kernel timing (wa_profile_*)
@@ -233,7 +239,7 @@ struct wa_model {
     for (auto& l : enc)
       for (wq4_tensor* t : {l.qkv, l.out, l.fc1, l.fc2}) wq4_tensor_destroy(t);
     for (auto& l : dec)
-      for (wq4_tensor* t : {l.qkv, l.out, l.cq, l.ckv, l.cout, l.fc1, l.fc2}) wq4_tensor_destroy(t);
+      for (wq4_tensor* t : {l.qkv, l.out, l.cq, l.cout, l.fc1, l.fc2}) wq4_tensor_destroy(t);
   }
 };
 
@@ -398,6 +404,26 @@ struct Builder {
     m->bytes += wq4_tensor_device_bytes(t);
     return t;
   }
+  // One linear weight [rows, k] uploaded in its raw GGUF form (Q4_0 blocks,
+  // or f16 halves for an F16 model) for kernels that dequantize it directly.
+  uint8_t* raw(const std::string& name, int rows, int k) {
+    if (st != WQ4_OK) return nullptr;
+    const size_t n = m->wtype == 1 ? (size_t)rows * k * 2 : (size_t)rows * k / 32 * 18;
+    std::vector<uint8_t> h(n);
+    const bool ok = m->wtype == 1 ? src.f16(name, rows, k, reinterpret_cast<uint16_t*>(h.data()))
+                                  : src.q4(name, rows, k, h.data());
+    if (!ok) {
+      st = fail(WQ4_EINVAL, src.err);
+      return nullptr;
+    }
+    uint8_t* p = m->dev.alloc<uint8_t>(n);
+    if (!p || hipMemcpy(p, h.data(), n, hipMemcpyHostToDevice) != hipSuccess) {
+      st = fail(WQ4_ENOMEM, "upload failed");
+      return nullptr;
+    }
+    m->bytes += n;
+    return p;
+  }
   // bias vector of a fused projection: absent biases (attention key) are 0.
   float* bias_cat(const std::vector<std::string>& names, int n) {
     std::vector<float> v;
@@ -470,9 +496,11 @@ wq4_status build_model(wa_model* m, Source& src) {
     L.ln2_b = B.vec(p + ".cross_attn_ln.bias", Dt, -0.05f, 0.05f);
     L.cq = B.q4({p + ".cross_attn.query.weight"}, {Dt}, Dt);
     L.cq_b = B.vec(p + ".cross_attn.query.bias", Dt, -0.02f, 0.02f);
-    // cross-attention key has no bias (loader.rs:205-210)
-    L.ckv = B.q4({p + ".cross_attn.key.weight", p + ".cross_attn.value.weight"}, {Dt, Dt}, D);
-    L.ckv_b = B.bias_cat({p + ".cross_attn.key.bias", p + ".cross_attn.value.bias"}, Dt);
+    // cross-attention key / value (loader.rs:205-210; the key bias, absent
+    // in Whisper, cancels in the softmax and is not needed)
+    L.ck_raw = B.raw(p + ".cross_attn.key.weight", Dt, D);
+    L.cv_raw = B.raw(p + ".cross_attn.value.weight", Dt, D);
+    L.cv_b = B.bias_cat({p + ".cross_attn.value.bias"}, Dt);
     L.cout = B.q4({p + ".cross_attn.out.weight"}, {Dt}, Dt);
     L.cout_b = B.vec(p + ".cross_attn.out.bias", Dt, -0.02f, 0.02f);
     L.ln3_w = B.vec(p + ".mlp_ln.weight", Dt, 0.9f, 1.1f);
@@ -508,12 +536,16 @@ wq4_status alloc_activations(wa_model* m) {
   m->qkv = f32(renc * 3 * D);
   m->at_d = tiled(renc, D);
   m->at_f = tiled(renc, F);
-  m->enc_at = tiled(renc, D);
+  m->enc_planes = d.alloc<_Float16>((size_t)renc * m->ns * D);
+  m->bytes += (size_t)renc * m->ns * D * 2;
   for (auto& L : m->dec) {
     L.cache_k = f32((int64_t)B * c.n_text_ctx * Dt);
     L.cache_v = f32((int64_t)B * c.n_text_ctx * Dt);
-    L.cross_kv = f32(renc * 2 * Dt);
   }
+  // cross-attention scratch, sized for the largest plan over 1..4B rows
+  const int HP = (c.n_text_head + 15) / 16 * 16;
+  size_t xpart = 0;
+  for (int r = 1; r <= rdec; ++r) xpart = std::max(xpart, wa::xattn_part_floats(r, c.n_text_head, Dt, T));
   m->groups.resize(kMaxGroups);
   for (DecGroup& g : m->groups) {  // each group sized for the whole batch (small)
     g.xd = f32(rdec * Dt);
@@ -529,26 +561,26 @@ wq4_status alloc_activations(wa_model* m) {
     g.ntok = d.alloc<int>(B);
     g.done = d.alloc<int>(B);
     g.state = d.alloc<wa::DecodeState>(1);
-    g.xattn_part = f32((int64_t)wa::cross_attention_part_floats(B, c.n_text_head, T));
-    g.xattn_counters = d.alloc<int>((size_t)B * c.n_text_head);
+    g.xattn_part = f32((int64_t)xpart);
+    g.xqt = d.alloc<_Float16>((size_t)rdec * m->ns * HP * Dt);
+    m->bytes += (size_t)rdec * m->ns * HP * Dt * 2;
     for (void* p : {(void*)g.xd, (void*)g.qkvd, (void*)g.qd, (void*)g.hid, (void*)g.logits, (void*)g.atd_dec,
                     (void*)g.atf_dec, (void*)g.prompt_tok, (void*)g.next_tok, (void*)g.tokens, (void*)g.ntok,
-                    (void*)g.done, (void*)g.state, (void*)g.xattn_part, (void*)g.xattn_counters})
+                    (void*)g.done, (void*)g.state, (void*)g.xattn_part, (void*)g.xqt})
       if (!p) return fail(WQ4_ENOMEM, "decode-group allocation failed");
-    WA_HIP(hipMemset(g.xattn_counters, 0, (size_t)B * c.n_text_head * sizeof(int)));
+    WA_HIP(hipMemset(g.xqt, 0, (size_t)rdec * m->ns * HP * Dt * 2));  // padded heads stay 0
     WA_HIP(hipMemset(g.atd_dec, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
     WA_HIP(hipMemset(g.atf_dec, 0, wq4_atiled_bytes(rdec, Ft, m->prec)));
     WA_HIP(hipHostMalloc(reinterpret_cast<void**>(&g.host_ndone), 8 * sizeof(int), 0));
     WA_HIP(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
   }
-  for (void* p : {(void*)m->h1, (void*)m->x, (void*)m->qkv, (void*)m->at_d, (void*)m->at_f, (void*)m->enc_at})
+  for (void* p : {(void*)m->h1, (void*)m->x, (void*)m->qkv, (void*)m->at_d, (void*)m->at_f, (void*)m->enc_planes})
     if (!p) return fail(WQ4_ENOMEM, "activation allocation failed");
   for (auto& L : m->dec)
-    if (!L.cache_k || !L.cache_v || !L.cross_kv) return fail(WQ4_ENOMEM, "KV cache allocation failed");
+    if (!L.cache_k || !L.cache_v) return fail(WQ4_ENOMEM, "KV cache allocation failed");
   // zero the A-tiled buffers once: padded rows stay finite forever
   WA_HIP(hipMemset(m->at_d, 0, wq4_atiled_bytes(renc, D, m->prec)));
   WA_HIP(hipMemset(m->at_f, 0, wq4_atiled_bytes(renc, F, m->prec)));
-  WA_HIP(hipMemset(m->enc_at, 0, wq4_atiled_bytes(renc, D, m->prec)));
   return WQ4_OK;
 }
 
@@ -581,8 +613,8 @@ Prof q4prof(wa_model* m, hipStream_t st, const wq4_tensor* w, int64_t rows) {
   return Prof(m, st, 0, 2.0 * rows * n * k * 1e-9, ((double)n * k * 18 / 32 + 4.0 * rows * k + 4.0 * rows * n) * 1e-9);
 }
 
-// WhisperEncoder::forward (encoder.rs:87-115) + ln_post into the A-tiled
-// operand of the cross-K/V projections.
+// WhisperEncoder::forward (encoder.rs:87-115) + ln_post (f32, into
+// enc_out_f32 or the conv scratch; m->enc_f32 points at it).
 wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st, float* enc_out_f32) {
   const Config& c = m->cfg;
   const int D = c.n_audio_state, T = c.n_audio_ctx, H = c.n_audio_head;
@@ -632,24 +664,21 @@ wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st,
   }
   {
     Prof p(m, st, 3, 0.0, ln_gb);
-    WA_WQ4(wq4_layernorm(m->x, m->lnp_w, m->lnp_b, rows, D, m->prec, m->enc_at, nullptr, st));
+    float* out = enc_out_f32 ? enc_out_f32 : m->h1;
+    WA_WQ4(wq4_layernorm(m->x, m->lnp_w, m->lnp_b, rows, D, WQ4_PREC_F16X2, nullptr, out, st));
+    m->enc_f32 = out;
   }
-  if (enc_out_f32) WA_WQ4(wq4_layernorm(m->x, m->lnp_w, m->lnp_b, rows, D, WQ4_PREC_F16X2, nullptr, enc_out_f32, st));
   return WQ4_OK;
 }
 
-// Cross-attention K/V of every decoder layer from encoder_out
-// (attention.rs:177-206 forward_init_cache, run once per clip).
+// The cross-attention state of every decoder layer: the reference caches
+// K = enc Wk^T and V = enc Wv^T per layer (attention.rs:177-206
+// forward_init_cache); here one copy of encoder_out as f16 planes serves all
+// layers (wa_xattn.hip).
 wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st) {
   const int64_t rows = (int64_t)B * m->cfg.n_audio_ctx;
   m->kv_batch = B;
-  for (auto& L : m->dec) {
-    Prof p = q4prof(m, st, L.ckv, rows);
-    // K|V written head-major [2][B][H][T][64]: each (clip, head) streams two
-    // contiguous 384 KB ranges in the decode steps' cross-attention
-    WA_WQ4(wq4_gemm_tiled_headmajor(L.ckv, L.ckv_b, m->enc_at, L.cross_kv, rows, m->cfg.n_audio_ctx,
-                                    m->cfg.n_text_state, m->prec, 1, st));
-  }
+  WA_HIP(wa::launch_enc_planes(m->enc_f32, rows, m->cfg.n_audio_state, m->ns, m->enc_planes, st));
   return WQ4_OK;
 }
 
@@ -663,7 +692,7 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
   const int B = g.nb;
   const int64_t rows = (int64_t)B * Tq;
   const size_t self_ofs = (size_t)g.b0 * H * c.n_text_ctx * 64;
-  const size_t cross_ofs = (size_t)g.b0 * H * T * 64, cross_v = (size_t)m->kv_batch * H * T * 64;
+  const _Float16* enc = m->enc_planes + (size_t)g.b0 * T * m->ns * c.n_audio_state;
   WA_HIP(wa::launch_embed(tokens, m->tok_emb, m->dec_pos, B, Tq, D, state, pos0, g.xd, st));
   for (auto& L : m->dec) {  // DecoderBlock (decoder.rs:77-112 / 140-183)
     WA_WQ4(wq4_layernorm(g.xd, L.ln1_w, L.ln1_b, rows, D, m->prec, g.atd_dec, nullptr, st));
@@ -673,8 +702,8 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
     WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
     WA_WQ4(wq4_layernorm(g.xd, L.ln2_w, L.ln2_b, rows, D, m->prec, g.atd_dec, nullptr, st));
     WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, g.atd_dec, nullptr, g.qd, nullptr, rows, 0u, m->prec, 2, st));
-    WA_HIP(wa::launch_cross_attention(g.qd, L.cross_kv + cross_ofs, L.cross_kv + cross_v + cross_ofs, B, Tq, T, H,
-                                      g.xattn_part, g.xattn_counters, g.atd_dec, m->ns, st));
+    WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_b, m->wtype, enc, B, Tq, T, H, D, g.xqt, g.xattn_part,
+                            g.atd_dec, m->ns, st));
     WA_WQ4(wq4_gemm_tiled(L.cout, L.cout_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
     WA_WQ4(wq4_layernorm(g.xd, L.ln3_w, L.ln3_b, rows, D, m->prec, g.atd_dec, nullptr, st));
     WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, g.atd_dec, nullptr, nullptr, g.atf_dec, rows,
@@ -1126,23 +1155,25 @@ wq4_status wa_probe_kernels(wa_model* m, int n_clips, int iters, double* out) {
   const int B = n_clips, D = c.n_text_state, T = c.n_audio_ctx, H = c.n_text_head;
   DecLayer& L = m->dec[0];
   DecGroup& g = m->groups[0];
-  const float* kb = L.cross_kv;
-  const float* vb = L.cross_kv + (size_t)m->kv_batch * H * T * 64;
+  const _Float16* enc = m->enc_planes;
   hipEvent_t a, b;
   WA_HIP(hipEventCreate(&a));
   WA_HIP(hipEventCreate(&b));
   float ms = 0.0f;
-  // cross-attention of one decode step (Tq = 1): reads K and V of every clip
-  WA_HIP(wa::launch_cross_attention(g.qd, kb, vb, B, 1, T, H, g.xattn_part, g.xattn_counters, g.atd_dec, m->ns, st));
+  // cross-attention of one decode step (Tq = 1): streams every clip's encoder output
+  WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_b, m->wtype, enc, B, 1, T, H, D, g.xqt, g.xattn_part,
+                          g.atd_dec, m->ns, st));
   WA_HIP(hipEventRecord(a, st));
   for (int i = 0; i < iters; ++i)
-    WA_HIP(wa::launch_cross_attention(g.qd, kb, vb, B, 1, T, H, g.xattn_part, g.xattn_counters, g.atd_dec, m->ns,
-                                      st));
+    WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_b, m->wtype, enc, B, 1, T, H, D, g.xqt, g.xattn_part,
+                            g.atd_dec, m->ns, st));
   WA_HIP(hipEventRecord(b, st));
   WA_HIP(hipEventSynchronize(b));
   WA_HIP(hipEventElapsedTime(&ms, a, b));
   out[0] = ms * 1e3 / iters;
-  out[1] = (double)B * T * 2 * D * 4 + (double)B * D * (4 + 2 * m->ns);
+  // algorithmic bytes: encoder output planes of every clip + Wk, Wv (raw) + q + output operand
+  const double wbytes = m->wtype == 1 ? 2.0 * D * D * 2 : 2.0 * D * D * 18 / 32;
+  out[1] = (double)B * T * D * 2 * m->ns + wbytes + (double)B * D * (4 + 2 * m->ns);
   // fc1 of one decode step (M = n_clips rows, decode kernel, GELU + tiled out)
   const int F = 4 * D;
   WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, g.atd_dec, nullptr, nullptr, g.atf_dec, B, WQ4_EPI_GELU | WQ4_EPI_TILED_OUT,
@@ -1159,6 +1190,31 @@ wq4_status wa_probe_kernels(wa_model* m, int n_clips, int iters, double* out) {
   out[4] = 2.0 * B * F * D;
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
+  return WQ4_OK;
+}
+
+wq4_status wa_xattn_check(int device, const float* q_dev, const uint8_t* wk_dev, const uint8_t* wv_dev,
+                          const float* bv_dev, int weight_type, const float* enc_dev, int n_clips, int Tq, int T,
+                          int H, wq4_precision prec, float* out_dev) {
+  if (!q_dev || !wk_dev || !wv_dev || !bv_dev || !enc_dev || !out_dev) return fail(WQ4_EINVAL, "null argument");
+  if (n_clips < 1 || Tq < 1 || T < 1 || H < 1) return fail(WQ4_EINVAL, "bad sizes");
+  const int D = 64 * H, ns = prec == WQ4_PREC_F16 ? 1 : 2, R = n_clips * Tq;
+  const int HP = (H + 15) / 16 * 16;
+  WA_HIP(hipSetDevice(device));
+  Dev d;
+  auto* planes = d.alloc<_Float16>((size_t)n_clips * T * ns * D);
+  auto* qt = d.alloc<_Float16>((size_t)R * ns * HP * D);
+  auto* part = d.alloc<float>(wa::xattn_part_floats(R, H, D, T));
+  const size_t tb = wq4_atiled_bytes(R, D, prec);
+  auto* tiled = d.alloc<_Float16>(tb / 2);
+  if (!planes || !qt || !part || !tiled) return fail(WQ4_ENOMEM, "allocation failed");
+  WA_HIP(hipMemset(qt, 0, (size_t)R * ns * HP * D * 2));
+  WA_HIP(hipMemset(tiled, 0, tb));
+  WA_HIP(wa::launch_enc_planes(enc_dev, (int64_t)n_clips * T, D, ns, planes, nullptr));
+  WA_HIP(wa::launch_xattn(q_dev, wk_dev, wv_dev, bv_dev, weight_type, planes, n_clips, Tq, T, H, D, qt, part, tiled,
+                          ns, nullptr));
+  WA_HIP(wa::launch_untile(tiled, R, D, ns, out_dev, nullptr));
+  WA_HIP(hipDeviceSynchronize());
   return WQ4_OK;
 }
 

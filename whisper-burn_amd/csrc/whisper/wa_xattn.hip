@@ -1,0 +1,661 @@
+// wa_xattn.hip -- decoder cross-attention computed over the encoder output
+// itself (no per-layer cross K/V caches).
+//
+// Reference: CrossAttention::forward_with_cache (src/model/attention.rs:
+// 204-236) + scaled_dot_product_attention (:243-298):
+//     K = enc Wk^T + bk,  V = enc Wv^T + bv   (cached per layer, [T, D])
+//     out_h = softmax(q_h K_h^T / 8) V_h
+// Restated (exact in real arithmetic):
+//     qt_h  = Wk_h^T q_h / 8                        [D]    (xattn_q_kernel)
+//     s_t   = qt_h . enc_t     (q_h . bk_h is the same for every t: softmax-
+//                               invariant, dropped)
+//     Z_h   = sum_t softmax(s)_t enc_t              [D]    (xattn_main_kernel)
+//     out_h = Wv_h Z_h + bv_h  (softmax weights sum to 1) (xattn_out_kernel)
+// Every layer streams the clip's encoder output once -- T*D values shared by
+// all heads -- instead of its K and V (2*T*D), halving the HBM bytes of the
+// decode step's dominant kernel, and the 32 layers' K/V caches (15.7 GB for
+// 32 Large-V3 clips) and their projection GEMMs disappear.
+//
+// Numerics: enc and qt are f16 hi/lo pairs (x = hi + lo to 2^-22) and every
+// product runs as three f16 MFMAs (hi*hi + lo*hi + hi*lo, f32 accumulate) --
+// the f32-faithful arithmetic of the Q4 GEMMs; NS = 1 (WQ4_PREC_F16) keeps
+// only the hi planes.  Softmax is the online (flash) form in f32 with expf.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+
+#include "../wq4_device.hpp"
+#include "../wq4_lnmath.hpp"
+#include "wa_kernels.hpp"
+
+namespace wa {
+namespace {
+
+using wq4::atile_store4;
+using wq4::kbp_of;
+using wq4::split_f16;
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWtQ4 = 0, kWtF16 = 1;  // raw weight formats (wa_model wtype)
+constexpr int kTc = 16;          // keys (encoder frames) per sub-chunk
+constexpr int kMaxD = 1280;
+constexpr int kMaxSplits = 8;  // xattn_out_kernel keeps a column's split values in registers
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
+
+// gfx950: the K=32 / K=16 forms run at twice the FLOP rate of the older
+// 16x16x16 / 32x32x8 forms (same cycles per instruction, tools/mfma_cycles.hip)
+__device__ __forceinline__ floatx4 mfma16x32(half8 a, half8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ floatx16 mfma32x16(half8 a, half8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+// ds_read_b64_tr_b16 (cdna_hip_programming.md T10): per 16-lane group a 4-row
+// x 16-column block, lane i receiving column i (row q in element q)
+__device__ __forceinline__ half4 lds_tr4(const _Float16* p) {
+  return __builtin_bit_cast(half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+                                       (__attribute__((address_space(3))) fp16x4_t*)(p)));
+}
+
+// Weight element (o, c) of a [rows, K] linear weight in its raw GGUF form:
+// Q4_0 blocks (tests.rs:60-87: (nibble - 8) * d, f32) or f16.
+template <int WK>
+__device__ __forceinline__ void load_w32(const uint8_t* __restrict__ w, int K, int o, int kb, float* out) {
+  if (WK == kWtQ4) {
+    const uint16_t* blk = reinterpret_cast<const uint16_t*>(w + ((size_t)o * (K / 32) + kb) * 18);
+    const float d = (float)__builtin_bit_cast(_Float16, blk[0]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t two = blk[1 + i];  // bytes 2i, 2i+1 of the 16 nibble bytes
+      out[2 * i] = (float)((int)(two & 15u) - 8) * d;
+      out[2 * i + 1] = (float)((int)((two >> 8) & 15u) - 8) * d;
+      out[16 + 2 * i] = (float)((int)((two >> 4) & 15u) - 8) * d;
+      out[16 + 2 * i + 1] = (float)((int)((two >> 12) & 15u) - 8) * d;
+    }
+  } else {
+    const _Float16* p = reinterpret_cast<const _Float16*>(w) + (size_t)o * K + kb * 32;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) out[i] = (float)p[i];
+  }
+}
+
+// ------------------------------------------------------------- qt = Wk^T q --
+// grid (H, D / 64, ceil(R / 32)), 256 threads: 64 columns of one head for up
+// to 32 rows.  qt: [R][NS][HP][D] f16 planes (rows of padded heads h >= H
+// are never written: zeroed once at allocation).  Thread (row, 8 columns).
+template <int NS, int WK>
+__global__ __launch_bounds__(256) void xattn_q_kernel(const float* __restrict__ q, int R, int D,
+                                                      const uint8_t* __restrict__ wk, int HP,
+                                                      _Float16* __restrict__ qt) {
+  __shared__ __attribute__((aligned(16))) float wt[64][64 + 4];
+  __shared__ float qs[32][65];
+  const int h = blockIdx.x, c0 = blockIdx.y * 64, r0 = blockIdx.z * 32, tid = threadIdx.x;
+  float qv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int i = tid + k * 256, row = i >> 6, d = i & 63;
+    qv[k] = r0 + row < R ? q[(size_t)(r0 + row) * D + h * 64 + d] : 0.0f;
+  }
+  if (tid < 128) {  // 64 rows x 2 blocks of 32 columns
+    const int d = tid >> 1, blk = tid & 1;
+    float v[32];
+    load_w32<WK>(wk, D, h * 64 + d, (c0 >> 5) + blk, v);
+#pragma unroll
+    for (int i = 0; i < 32; i += 4)
+      *reinterpret_cast<floatx4*>(&wt[d][blk * 32 + i]) = floatx4{v[i], v[i + 1], v[i + 2], v[i + 3]};
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int i = tid + k * 256;
+    qs[i >> 6][i & 63] = qv[k];
+  }
+  __syncthreads();
+  const int rr = tid >> 3, cc = (tid & 7) * 8;
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
+#pragma unroll 4
+  for (int d = 0; d < 64; ++d) {
+    const floatx4 w0 = *reinterpret_cast<const floatx4*>(&wt[d][cc]);
+    const floatx4 w1 = *reinterpret_cast<const floatx4*>(&wt[d][cc + 4]);
+    const float qq = qs[rr][d];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[i] = fmaf(qq, w0[i], acc[i]);
+      acc[4 + i] = fmaf(qq, w1[i], acc[4 + i]);
+    }
+  }
+  const int r = r0 + rr;
+  if (r < R) {
+    half8 hi, lo;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      _Float16 x, y;
+      split_f16(acc[i] * 0.125f, x, y);  // / sqrt(64) (attention.rs:262), exact
+      hi[i] = x;
+      lo[i] = y;
+    }
+    *reinterpret_cast<half8*>(qt + (((size_t)r * NS + 0) * HP + h) * D + c0 + cc) = hi;
+    if (NS == 2) *reinterpret_cast<half8*>(qt + (((size_t)r * NS + 1) * HP + h) * D + c0 + cc) = lo;
+  }
+}
+
+// ------------------------------------------------------------ main stream --
+// grid (S, R), NW waves; wave w owns columns [w*D/NW, (w+1)*D/NW).
+// Per sub-chunk of 16 frames: the frames' enc rows go to LDS; scores
+// S[t][h] = sum_c enc[t][c] qt[h][c] (16x16x32 MFMA, m = frame, n = head,
+// per-wave column slice, summed over waves through LDS); online softmax per
+// head; Z[h][c] += P[h][t] enc[t][c] (32x32x16 MFMA, m = the 32 padded
+// heads, k = the 16 frames read transposed from the same LDS image by
+// ds_read_b64_tr_b16; accumulators stay in registers).  Writes per (row,
+// split): Z [H][D] and (max, sum) [H].
+template <int D, int HT, int NS, int NW, int PF>
+__global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __restrict__ qt,
+                                                             const _Float16* __restrict__ enc, int Tq, int T,
+                                                             int H, int S, int CH, float* __restrict__ zpart,
+                                                             float* __restrict__ mlpart) {
+  constexpr int kThreads = 64 * NW;
+  constexpr int CW = D / NW;      // columns per wave
+  constexpr int KS = CW / 32;     // 32-column steps per wave (score k-steps = Z column tiles)
+  constexpr int HP = HT * 16;     // padded heads of the score tiles
+  constexpr int ROW = NS * D;     // halves per encoder row (hi plane | lo plane)
+  constexpr int RS = ROW + 32;    // LDS row stride: == 16 dwords (mod 64) -> conflict-free transposed reads
+  constexpr int NV = kTc * ROW / 8;  // 16-byte vectors per sub-chunk
+  constexpr int NLD = (NV + kThreads - 1) / kThreads;
+  constexpr int HR = HT == 2 ? 1 : HT;  // score head tiles held in registers
+  static_assert(CW * NW == D && CW % 32 == 0 && HT <= 2 && (PF == 1 || PF == 2), "bad column split");
+  __shared__ __attribute__((aligned(16))) _Float16 se[kTc * RS];
+  __shared__ float red[NW][HT][16][17];
+  __shared__ __attribute__((aligned(16))) _Float16 sp[NS][32][kTc];
+  __shared__ float salpha[32];
+  __shared__ __attribute__((aligned(16))) _Float16 sq1[HT == 2 ? NS : 1][4][HT == 2 ? D + 16 : 8];
+
+  const int s = blockIdx.x, r = blockIdx.y;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int l16 = l & 15, lq = l >> 4, l32 = l & 31, lh = l >> 5;
+  const _Float16* E = enc + (size_t)(r / Tq) * T * ROW;
+  const int c0 = w * CW;
+  const int ts = s * CH * kTc;
+  const int te = min(T, ts + CH * kTc);
+  const int nch = te > ts ? (te - ts + kTc - 1) / kTc : 0;
+
+  // qt operands (B of the score MFMA: k = column, n = head): head tile 0 in
+  // registers; for H in (16, 20] the 4 heads of tile 1 from LDS (registers of
+  // a mostly-padding tile would not fit beside the Z accumulators)
+  half8 qb[HR][KS][NS];
+#pragma unroll
+  for (int ht = 0; ht < HR; ++ht)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int p = 0; p < NS; ++p)
+        qb[ht][ks][p] = *reinterpret_cast<const half8*>(
+            qt + (((size_t)r * NS + p) * HP + ht * 16 + l16) * D + c0 + ks * 32 + 8 * lq);
+  if (HT == 2) {
+    for (int i = tid; i < NS * 4 * (D / 8); i += kThreads) {
+      const int p = i / (4 * (D / 8)), rem = i - p * 4 * (D / 8), hr = rem / (D / 8), c8 = rem - hr * (D / 8);
+      *reinterpret_cast<half8*>(&sq1[p][hr][8 * c8]) =
+          *reinterpret_cast<const half8*>(qt + (((size_t)r * NS + p) * HP + 16 + hr) * D + 8 * c8);
+    }
+  }
+  // rows of P past the score tiles stay 0, their alpha 1
+  for (int i = tid; i < NS * 32 * kTc; i += kThreads) (&sp[0][0][0])[i] = (_Float16)0.0f;
+  if (tid < 32) salpha[tid] = 1.0f;
+
+  floatx16 zacc[KS];
+#pragma unroll
+  for (int ct = 0; ct < KS; ++ct)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) zacc[ct][j] = 0.0f;
+  // softmax state: thread owns (head, frame) entries tid + e * kThreads
+  constexpr int SMX = (HT * 256 + kThreads - 1) / kThreads;
+  float M[SMX], L[SMX];
+#pragma unroll
+  for (int e = 0; e < SMX; ++e) {
+    M[e] = -INFINITY;
+    L[e] = 0.0f;
+  }
+
+  // this range's frames through a buffer resource: rows past te (and the
+  // tail vectors when NV % threads != 0) read as zeros, no branches.  PF
+  // sub-chunks are in flight in registers while one is computed from LDS.
+  typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<_Float16*>(E + (size_t)ts * ROW), 0, nch > 0 ? (te - ts) * ROW * 2 : 0, 0x00020000);
+  auto fetch = [&](u32x4v (&buf)[NLD], int chi) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int v = tid + i * kThreads;
+      const int row = v / (ROW / 8), col = v - row * (ROW / 8);
+      const uint32_t off = v < NV ? (uint32_t)((chi * kTc + row) * ROW * 2 + col * 16) : 0x7fffff00u;
+      buf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    }
+  };
+
+  // transposed-read lane geometry (Z phase): 16-lane group g reads rows
+  // 8*(g>>1) + 4*half + (0..3), columns 16*(g&1) + (0..15) of a 32-column
+  // tile; lane 4q+pp addresses row q, columns 4pp..4pp+3
+  const int g = l >> 4, gi = l & 15;
+  const int trow = 8 * (g >> 1) + (gi >> 2), tcol = 16 * (g & 1) + 4 * (gi & 3);
+
+  auto step = [&](u32x4v (&buf)[NLD], int chi) {
+    const int t0 = ts + chi * kTc;
+    __syncthreads();  // previous sub-chunk's readers are done with se / sp
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int v = tid + i * kThreads;
+      const int row = v / (ROW / 8), col = v - row * (ROW / 8);
+      if (v < NV) *reinterpret_cast<u32x4v*>(&se[row * RS + col * 8]) = buf[i];
+    }
+    __syncthreads();
+    if (chi + PF < nch) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
+
+    // scores of this wave's column slice: A = enc (m = frame, k = column),
+    // B = qt (k = column, n = head)
+    floatx4 sacc[HT];
+#pragma unroll
+    for (int ht = 0; ht < HT; ++ht) sacc[ht] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      half8 a[NS];
+#pragma unroll
+      for (int p = 0; p < NS; ++p)
+        a[p] = *reinterpret_cast<const half8*>(&se[l16 * RS + p * D + c0 + ks * 32 + 8 * lq]);
+#pragma unroll
+      for (int ht = 0; ht < HT; ++ht) {
+        half8 b[NS];
+#pragma unroll
+        for (int p = 0; p < NS; ++p) {
+          if (ht < HR) {
+            b[p] = qb[ht < HR ? ht : 0][ks][p];
+          } else {
+            b[p] = half8{0, 0, 0, 0, 0, 0, 0, 0};
+            if (l16 < 4) b[p] = *reinterpret_cast<const half8*>(&sq1[p][l16 & 3][c0 + ks * 32 + 8 * lq]);
+          }
+        }
+        sacc[ht] = mfma16x32(a[0], b[0], sacc[ht]);
+        if (NS == 2) {
+          sacc[ht] = mfma16x32(a[1], b[0], sacc[ht]);
+          sacc[ht] = mfma16x32(a[0], b[1], sacc[ht]);
+        }
+      }
+    }
+#pragma unroll
+    for (int ht = 0; ht < HT; ++ht)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[w][ht][l16][4 * lq + j] = sacc[ht][j];
+    __syncthreads();
+
+    // online softmax: entry (head tile, head, frame); 16 lanes per head
+#pragma unroll
+    for (int e = 0; e < SMX; ++e) {
+      const int idx = tid + e * kThreads;
+      if (idx < HT * 256) {
+        const int ht = idx >> 8, hh = (idx >> 4) & 15, t = idx & 15;
+        const int h = ht * 16 + hh;
+        float sv = 0.0f;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) sv += red[ww][ht][hh][t];
+        const bool valid = h < H && t0 + t < te;
+        sv = valid ? sv : -INFINITY;
+        float cm = sv;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
+        const float mn = fmaxf(M[e], cm);
+        float alpha = 1.0f, p = 0.0f;
+        if (mn != -INFINITY) {
+          alpha = expf(M[e] - mn);
+          p = valid ? expf(sv - mn) : 0.0f;
+        }
+        float ps = p;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) ps += __shfl_xor(ps, o, 64);
+        L[e] = L[e] * alpha + ps;
+        M[e] = mn;
+        _Float16 phi, plo;
+        split_f16(p, phi, plo);
+        sp[0][h][t] = phi;
+        if (NS == 2) sp[1][h][t] = plo;
+        if (t == 0) salpha[h] = alpha;
+      }
+    }
+    __syncthreads();
+
+    // Z update: A = P (m = head, k = frame), B = enc (k = frame, n = column)
+    half8 pa[NS];
+#pragma unroll
+    for (int p = 0; p < NS; ++p) pa[p] = *reinterpret_cast<const half8*>(&sp[p][l32][8 * lh]);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float al = salpha[(j & 3) + 8 * (j >> 2) + 4 * lh];
+#pragma unroll
+      for (int ct = 0; ct < KS; ++ct) zacc[ct][j] *= al;
+    }
+#pragma unroll
+    for (int ct = 0; ct < KS; ++ct) {
+      half8 eb[NS];
+#pragma unroll
+      for (int p = 0; p < NS; ++p) {
+        const _Float16* base = &se[trow * RS + p * D + c0 + ct * 32 + tcol];
+        const half4 x0 = lds_tr4(base);
+        const half4 x1 = lds_tr4(base + 4 * RS);
+        eb[p] = half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+      }
+      zacc[ct] = mfma32x16(pa[0], eb[0], zacc[ct]);
+      if (NS == 2) {
+        zacc[ct] = mfma32x16(pa[1], eb[0], zacc[ct]);
+        zacc[ct] = mfma32x16(pa[0], eb[1], zacc[ct]);
+      }
+    }
+  };
+
+  u32x4v pre0[NLD];
+  u32x4v pre1[PF == 2 ? NLD : 1];
+  if (nch > 0) fetch(pre0, 0);
+  if constexpr (PF == 2) {
+    if (nch > 1) fetch(pre1, 1);
+    for (int chi = 0; chi < nch; chi += 2) {
+      step(pre0, chi);
+      if (chi + 1 < nch) step(pre1, chi + 1);
+    }
+  } else {
+    for (int chi = 0; chi < nch; ++chi) step(pre0, chi);
+  }
+
+  // partials of this (row, split)
+  const size_t base = (size_t)r * S + s;
+#pragma unroll
+  for (int e = 0; e < SMX; ++e) {
+    const int idx = tid + e * kThreads;
+    if (idx < HT * 256 && (idx & 15) == 0) {
+      const int h = (idx >> 8) * 16 + ((idx >> 4) & 15);
+      if (h < H) {
+        mlpart[(base * H + h) * 2] = M[e];
+        mlpart[(base * H + h) * 2 + 1] = L[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int h = (j & 3) + 8 * (j >> 2) + 4 * lh;
+    if (h < H) {
+#pragma unroll
+      for (int ct = 0; ct < KS; ++ct) zpart[(base * H + h) * D + c0 + ct * 32 + l32] = zacc[ct][j];
+    }
+  }
+}
+
+// ------------------------------------------------------ merge the splits --
+// grid (ceil(D / 256), H, R), 256 threads: Zn[r][h][c] = sum_s w_s Z_s[c],
+// w_s = exp(M_s - max) / sum_s' exp(M_s' - max) L_s' (the flash-attention
+// merge of the S frame ranges), for 256 columns per workgroup: the partial
+// stream is spread over many workgroups.
+__global__ __launch_bounds__(256) void xattn_merge_kernel(const float* __restrict__ zpart,
+                                                          const float* __restrict__ mlpart, int R, int H, int D,
+                                                          int S, float* __restrict__ zn) {
+  const int h = blockIdx.y, r = blockIdx.z, c = blockIdx.x * 256 + threadIdx.x;
+  float m[kMaxSplits], lv[kMaxSplits], zv[kMaxSplits];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < kMaxSplits; ++s) {
+    m[s] = -INFINITY;
+    lv[s] = 0.0f;
+    zv[s] = 0.0f;
+    if (s < S) {
+      const size_t b = ((size_t)r * S + s) * H + h;
+      m[s] = mlpart[b * 2];
+      lv[s] = mlpart[b * 2 + 1];
+      if (c < D) zv[s] = zpart[b * D + c];
+    }
+    mx = fmaxf(mx, m[s]);
+  }
+  float lsum = 0.0f, acc = 0.0f;
+#pragma unroll
+  for (int s = 0; s < kMaxSplits; ++s) {
+    const float a = m[s] == -INFINITY ? 0.0f : expf(m[s] - mx);
+    lsum = fmaf(a, lv[s], lsum);
+    acc = fmaf(a, zv[s], acc);
+  }
+  if (c < D) zn[((size_t)r * H + h) * D + c] = acc / lsum;
+}
+
+// ------------------------------------------------------- out = Wv Zn + bv --
+// grid (H, ceil(R / 4)), 512 threads: the head's 64 raw Wv rows (46 KB of
+// Q4_0 blocks) and 4 rows of Zn ([column] x 4 rows) in LDS; thread (row pair
+// d, d + 32; blocks b, b + 16, b + 32) dequantizes each block once for the 4
+// rows; 16 block-group partials per output are added through LDS and
+// out[r][h*64 + d] + bv goes into the A-tiled operand of the output
+// projection.
+template <int NS, int WK>
+__global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict__ zn, int R, int H, int D,
+                                                        const uint8_t* __restrict__ wv,
+                                                        const float* __restrict__ bv, _Float16* __restrict__ tiled) {
+  constexpr int kStage = WK == kWtQ4 ? 64 * (kMaxD / 32) * 18 : 16;  // 46 KB of Q4 blocks
+  __shared__ __attribute__((aligned(16))) uint8_t sw[kStage];
+  __shared__ __attribute__((aligned(16))) floatx4 zs[kMaxD];  // [column] x 4 rows
+  __shared__ float red[16][64][5];
+  const int h = blockIdx.x, r0 = blockIdx.y * 4, tid = threadIdx.x;
+  const int nkb = D / 32;
+  const size_t rowbytes = (size_t)nkb * 18;
+  if (WK == kWtQ4) {  // the head's 64 rows are contiguous: 64 * nkb * 18 bytes in 16-B chunks
+    const uint8_t* src = wv + (size_t)h * 64 * rowbytes;
+    const int n16 = (int)(64 * rowbytes / 16);
+    for (int i = tid; i < n16; i += 512)
+      *reinterpret_cast<uint4*>(&sw[i * 16]) = *reinterpret_cast<const uint4*>(src + (size_t)i * 16);
+  }
+  for (int c = tid; c < D; c += 512) {
+    floatx4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = r0 + j < R ? zn[((size_t)(r0 + j) * H + h) * D + c] : 0.0f;
+    zs[c] = v;
+  }
+  __syncthreads();
+  const int dp = tid & 31, bg = tid >> 5;  // rows dp, dp + 32; blocks bg, bg + 16, bg + 32
+  floatx4 acc0{0.0f, 0.0f, 0.0f, 0.0f}, acc1{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 1
+  for (int kb = bg; kb < nkb; kb += 16) {
+    if (WK == kWtQ4) {
+      // word i of the 16 nibble bytes holds elements 2i, 2i+1 (low nibbles)
+      // and 16+2i, 17+2i (high nibbles) of the block
+      const uint16_t* b0 = reinterpret_cast<const uint16_t*>(&sw[(size_t)dp * rowbytes + (size_t)kb * 18]);
+      const uint16_t* b1 = reinterpret_cast<const uint16_t*>(&sw[(size_t)(dp + 32) * rowbytes + (size_t)kb * 18]);
+      const float d0 = (float)__builtin_bit_cast(_Float16, b0[0]);
+      const float d1 = (float)__builtin_bit_cast(_Float16, b1[0]);
+#pragma unroll 2
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t t0 = b0[1 + i], t1 = b1[1 + i];
+        const int e[4] = {2 * i, 2 * i + 1, 16 + 2 * i, 17 + 2 * i};
+        const int sh[4] = {0, 8, 4, 12};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float wa = (float)((int)((t0 >> sh[q]) & 15u) - 8) * d0;
+          const float wb = (float)((int)((t1 >> sh[q]) & 15u) - 8) * d1;
+          const floatx4 z = zs[kb * 32 + e[q]];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc0[j] = fmaf(wa, z[j], acc0[j]);
+            acc1[j] = fmaf(wb, z[j], acc1[j]);
+          }
+        }
+      }
+    } else {
+      float w0[32], w1[32];
+      load_w32<WK>(wv, D, h * 64 + dp, kb, w0);
+      load_w32<WK>(wv, D, h * 64 + dp + 32, kb, w1);
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        const floatx4 z = zs[kb * 32 + i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc0[j] = fmaf(w0[i], z[j], acc0[j]);
+          acc1[j] = fmaf(w1[i], z[j], acc1[j]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[bg][dp][j] = acc0[j];
+    red[bg][dp + 32][j] = acc1[j];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int j = tid >> 4, d0 = 4 * (tid & 15), r = r0 + j;
+    if (r < R) {
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sacc = bv[h * 64 + d0 + i];
+#pragma unroll
+        for (int g = 0; g < 16; ++g) sacc += red[g][d0 + i][j];
+        o[i] = sacc;
+      }
+      atile_store4<NS>(tiled, r, h * 64 + d0, kbp_of(D), o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+// f32 rows [rows][D] -> [rows][NS][D] f16 planes (hi | lo)
+template <int NS>
+__global__ __launch_bounds__(256) void enc_planes_kernel(const float* __restrict__ x, int64_t n, int D,
+                                                         _Float16* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t row = i / D;
+  const int c = (int)(i - row * D);
+  _Float16 hi, lo;
+  split_f16(x[i], hi, lo);
+  out[(row * NS) * D + c] = hi;
+  if (NS == 2) out[(row * NS + 1) * D + c] = lo;
+}
+
+// 8 waves (4 when D / 8 is not a multiple of 32: D = 384)
+// A-tiled operand rows [R][K] -> f32 (diagnostics)
+template <int NS>
+__global__ __launch_bounds__(256) void untile_kernel(const _Float16* __restrict__ t, int R, int K,
+                                                     float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= R * K) return;
+  const int r = i / K, k = i - r * K;
+  float v = (float)t[wq4::atile_index(r, k, kbp_of(K), NS, 0)];
+  if (NS == 2) v += (float)t[wq4::atile_index(r, k, kbp_of(K), NS, 1)];
+  out[i] = v;
+}
+
+// 8 waves (two per SIMD, 256 registers each: the Z accumulators of an
+// eighth of the columns + one sub-chunk in flight); 4 when D / 8 is not a
+// multiple of 32 (D = 384).  A second sub-chunk in flight (PF = 2) does not
+// fit the register file at Large-V3 f16x2.
+template <int D, int HT, int NS>
+void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T, int H, int S, int CH, float* z,
+                 float* ml, hipStream_t st) {
+  constexpr int NW = (D / 8) % 32 == 0 ? 8 : 4, PF = 1;
+  hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, NW, PF>), g, dim3(64 * NW), 0, st, qt, enc, Tq, T, H, S, CH, z,
+                     ml);
+}
+
+}  // namespace
+
+// The frame split depends on T only -- never on the number of query rows --
+// so every row's arithmetic (and its tokens) is independent of the batch.
+// 8 ranges of 12 sub-chunks for T = 1500: 256 workgroups at 32 rows.
+XattnPlan xattn_plan(int R, int T) {
+  (void)R;
+  const int nchunk = (T + kTc - 1) / kTc;
+  int S = 8;
+  if (const char* e = getenv("WA_XATTN_SPLITS")) S = atoi(e);
+  S = std::max(1, std::min({S, nchunk, kMaxSplits}));
+  XattnPlan p;
+  p.ch = (nchunk + S - 1) / S;
+  p.splits = (nchunk + p.ch - 1) / p.ch;
+  return p;
+}
+
+size_t xattn_part_floats(int R, int H, int D, int T) {
+  const XattnPlan p = xattn_plan(R, T);
+  return (size_t)R * p.splits * H * ((size_t)D + 2) + (size_t)R * H * D;
+}
+
+hipError_t launch_untile(const _Float16* tiled, int R, int K, int ns, float* out, hipStream_t st) {
+  const dim3 g((R * K + 255) / 256);
+  if (ns == 2)
+    hipLaunchKernelGGL(untile_kernel<2>, g, dim3(256), 0, st, tiled, R, K, out);
+  else
+    hipLaunchKernelGGL(untile_kernel<1>, g, dim3(256), 0, st, tiled, R, K, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_planes(const float* x, int64_t rows, int D, int ns, _Float16* out, hipStream_t st) {
+  const int64_t n = rows * D;
+  const dim3 g((unsigned)((n + 255) / 256));
+  if (ns == 2)
+    hipLaunchKernelGGL(enc_planes_kernel<2>, g, dim3(256), 0, st, x, n, D, out);
+  else
+    hipLaunchKernelGGL(enc_planes_kernel<1>, g, dim3(256), 0, st, x, n, D, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, const float* bv, int wtype,
+                        const _Float16* enc, int B, int Tq, int T, int H, int D, _Float16* qt, float* part,
+                        _Float16* tiled, int ns, hipStream_t st) {
+  const int R = B * Tq;
+  const int HT = (H + 15) / 16, HP = HT * 16;
+  if (D != H * 64 || D % 128 != 0 || D > kMaxD || H > 20) return hipErrorInvalidValue;
+  const XattnPlan p = xattn_plan(R, T);
+  float* z = part;
+  float* ml = part + (size_t)R * p.splits * H * D;
+  // qt = Wk^T q / 8
+  const dim3 gq(H, D / 64, (R + 31) / 32);
+  if (wtype == kWtQ4) {
+    if (ns == 2)
+      hipLaunchKernelGGL((xattn_q_kernel<2, kWtQ4>), gq, dim3(256), 0, st, q, R, D, wk, HP, qt);
+    else
+      hipLaunchKernelGGL((xattn_q_kernel<1, kWtQ4>), gq, dim3(256), 0, st, q, R, D, wk, HP, qt);
+  } else {
+    if (ns == 2)
+      hipLaunchKernelGGL((xattn_q_kernel<2, kWtF16>), gq, dim3(256), 0, st, q, R, D, wk, HP, qt);
+    else
+      hipLaunchKernelGGL((xattn_q_kernel<1, kWtF16>), gq, dim3(256), 0, st, q, R, D, wk, HP, qt);
+  }
+  // stream the encoder output
+  const dim3 gm(p.splits, R);
+#define WA_XMAIN(DD, HH)                                                          \
+  if (D == DD && HT == HH) {                                                      \
+    if (ns == 2)                                                                  \
+      launch_main<DD, HH, 2>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, st);   \
+    else                                                                          \
+      launch_main<DD, HH, 1>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, st);   \
+  } else
+  WA_XMAIN(1280, 2)
+  WA_XMAIN(1024, 1)
+  WA_XMAIN(768, 1)
+  WA_XMAIN(512, 1)
+  WA_XMAIN(384, 1)
+  return hipErrorInvalidValue;
+#undef WA_XMAIN
+  // merge the splits, then project with Wv into the output projection's operand
+  float* zn = ml + (size_t)R * p.splits * H * 2;
+  hipLaunchKernelGGL(xattn_merge_kernel, dim3((D + 255) / 256, H, R), dim3(256), 0, st, z, ml, R, H, D, p.splits,
+                     zn);
+  const dim3 go(H, (R + 3) / 4);
+  if (wtype == kWtQ4) {
+    if (ns == 2)
+      hipLaunchKernelGGL((xattn_out_kernel<2, kWtQ4>), go, dim3(512), 0, st, zn, R, H, D, wv, bv, tiled);
+    else
+      hipLaunchKernelGGL((xattn_out_kernel<1, kWtQ4>), go, dim3(512), 0, st, zn, R, H, D, wv, bv, tiled);
+  } else {
+    if (ns == 2)
+      hipLaunchKernelGGL((xattn_out_kernel<2, kWtF16>), go, dim3(512), 0, st, zn, R, H, D, wv, bv, tiled);
+    else
+      hipLaunchKernelGGL((xattn_out_kernel<1, kWtF16>), go, dim3(512), 0, st, zn, R, H, D, wv, bv, tiled);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace wa

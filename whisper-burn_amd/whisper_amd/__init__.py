@@ -65,7 +65,8 @@ def lib() -> ctypes.CDLL:
         L.wa_gguf_tensor_data.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t]
         L.wa_log_mel.argtypes = [c_int, vp, c_int, c_i64, c_i64, c_int, vp, vp]
         L.wa_mel_filterbank.argtypes = [c_int, f32p, f32p]
-        for n in ("wa_log_mel", "wa_mel_filterbank", "wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
+        L.wa_xattn_check.argtypes = [c_int, vp, vp, vp, vp, c_int, vp, c_int, c_int, c_int, c_int, c_int, vp]
+        for n in ("wa_xattn_check", "wa_log_mel", "wa_mel_filterbank", "wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
                   "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read", "wa_probe_kernels",
                   "wa_model_create_from_gguf", "wa_model_create_synthetic_ex", "wa_gguf_open", "wa_gguf_tensor_info", "wa_gguf_tensor_data"):
             getattr(L, n).restype = c_int
@@ -121,6 +122,21 @@ def log_mel(audio, n_mels: int = 128, n_samples: Optional[int] = None, out=None)
     check(lib().wa_log_mel(dev, ctypes.c_void_p(audio.data_ptr()), B, n, audio.stride(0), n_mels,
                            ctypes.c_void_p(out.data_ptr()),
                            ctypes.c_void_p(torch.cuda.current_stream(audio.device).cuda_stream)))
+    return out
+
+
+def xattn_check(q, wk_raw, wv_raw, bv, enc, Tq: int, H: int, weight_type: int = 0,
+                precision: int = wq4.PREC_F16X2):
+    """One decoder layer's cross-attention through the product kernels
+    (wa_xattn_check): q cuda f32 [B*Tq, 64H], wk_raw / wv_raw cuda uint8 raw
+    weights, bv cuda f32 [64H], enc cuda f32 [B, T, 64H] -> [B*Tq, 64H]."""
+    torch = _torch()
+    B, T, D = enc.shape
+    out = torch.empty((B * Tq, D), device=enc.device, dtype=torch.float32)
+    dev = enc.device.index if enc.device.index is not None else 0
+    ptr = lambda t: ctypes.c_void_p(t.contiguous().data_ptr())
+    check(lib().wa_xattn_check(dev, ptr(q), ptr(wk_raw), ptr(wv_raw), ptr(bv), weight_type, ptr(enc), B, Tq, T, H,
+                               precision, ptr(out)))
     return out
 
 
