@@ -159,9 +159,24 @@ wq4_status wq4_linear_forward_tiled_out(const wq4_tensor* w, const float* bias_d
  * output f32 row-major y_dev, or, with WQ4_EPI_TILED_OUT, the A-tiled
  * operand at_out_dev of a following GEMM (K' = N; N % 32 == 0).           */
 #define WQ4_EPI_TILED_OUT 4u
+/* wq4_gemm_ln_tiled only: LayerNorm inside the decode GEMM (see there). */
+#define WQ4_EPI_LN_FUSED 8u
 wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void* at_dev, const float* residual_dev,
                           float* y_dev, void* at_out_dev, int64_t rows, unsigned flags, wq4_precision prec,
                           int kernel, void* stream);
+
+/* LayerNorm (layers.rs:12-32) of x rows [rows, K] f32 followed by the GEMM
+ * of wq4_gemm_tiled (same flags / outputs) -- the attn_ln / mlp_ln ->
+ * Q4Linear pairs of encoder.rs:37-49 and decoder.rs:77-112.  By default
+ * wq4_layernorm writes at_scratch_dev (wq4_atiled_bytes(rows, K, prec)) and
+ * the GEMM reads it.  With WQ4_EPI_LN_FUSED in flags and a decode-sized row
+ * count the LayerNorm runs inside the GEMM instead (the A operand built from
+ * x in registers, bit-identical to the two-step path; slower on MI355X for
+ * the Whisper shapes, where every n-tile repeats the row statistics). */
+wq4_status wq4_gemm_ln_tiled(const wq4_tensor* w, const float* bias_dev, const float* x_dev, const float* ln_w_dev,
+                             const float* ln_b_dev, void* at_scratch_dev, const float* residual_dev, float* y_dev,
+                             void* at_out_dev, int64_t rows, unsigned flags, wq4_precision prec, int kernel,
+                             void* stream);
 
 /* Allocate (once) the per-(device, stream) split-K workspace that small-M
  * GEMMs on `stream` use.  The first small-M GEMM on a stream does this

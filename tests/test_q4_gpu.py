@@ -382,6 +382,49 @@ def test_gemm_headmajor_layout(torch, policy):
                                              ctypes.c_void_p(hm.data_ptr()), m, 25, d, wq4.PREC_F16X2, policy, st))
 
 
+@pytest.mark.parametrize("wtype", ["q4_0", "f16"])
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("m,n,flags", [(1, 3840, 0), (17, 1280, 0), (32, 5120, 5), (100, 1280, 2), (128, 96, 0)])
+def test_gemm_ln_fused_bit_exact(torch, wtype, prec, m, n, flags):
+    """wq4_gemm_ln_tiled (LayerNorm built inside the decode GEMM) equals
+    wq4_layernorm -> wq4_gemm_tiled bit for bit (flags: 1 GELU, 2 residual,
+    4 tiled output)."""
+    import ctypes
+
+    k = 1280 if n != 96 else 160
+    rng = np.random.default_rng(m * 7 + n + prec)
+    if wtype == "f16":
+        t = wq4.Q4Tensor.from_f16((rng.standard_normal((n, k)) * 0.03).astype(np.float16))
+    else:
+        t = wq4.Q4Tensor.from_q4_bytes(oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.05).astype(np.float32)), [n, k])
+    x = to_dev(torch, (rng.standard_normal(m * k) * 2 + 0.5).astype(np.float32), (m, k))
+    g = to_dev(torch, rng.uniform(0.8, 1.2, k).astype(np.float32), (k,))
+    be = to_dev(torch, rng.uniform(-0.1, 0.1, k).astype(np.float32), (k,))
+    b = to_dev(torch, (rng.standard_normal(n) * 0.1).astype(np.float32), (n,))
+    res = to_dev(torch, rng.standard_normal(m * n).astype(np.float32), (m, n))
+    L = wq4.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    p = lambda a: ctypes.c_void_p(a.data_ptr()) if a is not None else None
+    atb = L.wq4_atiled_bytes(m, k, prec)
+    at_ref = torch.zeros(atb, dtype=torch.uint8, device="cuda:0")
+    at_scr = torch.zeros(atb, dtype=torch.uint8, device="cuda:0")
+    tiled = (flags & 4) != 0
+    ob = L.wq4_atiled_bytes(m, n, prec)
+    outs = []
+    for fused in (False, True):
+        y = torch.full((m, n), 7.0, device="cuda:0") if not tiled else None
+        ot = torch.zeros(ob, dtype=torch.uint8, device="cuda:0") if tiled else None
+        r = res if flags & 2 else None
+        if fused:
+            wq4.check(L.wq4_gemm_ln_tiled(t.handle, p(b), p(x), p(g), p(be), p(at_scr), p(r), p(y), p(ot), m,
+                                          flags | 8, prec, 2, st))  # WQ4_EPI_LN_FUSED
+        else:
+            wq4.check(L.wq4_layernorm(p(x), p(g), p(be), m, k, prec, p(at_ref), None, st))
+            wq4.check(L.wq4_gemm_tiled(t.handle, p(b), p(at_ref), p(r), p(y), p(ot), m, flags, prec, 2, st))
+        outs.append((y if not tiled else ot).cpu().numpy())
+    assert np.array_equal(outs[0].view(np.uint32) if not tiled else outs[0], outs[1].view(np.uint32) if not tiled else outs[1])
+
+
 # ------------------------------------------- f16 weights (BASELINE config 5) --
 @pytest.mark.parametrize("policy", [1, 2])
 @pytest.mark.parametrize("m,n,k", [(1, 1280, 1280), (32, 5120, 1280), (100, 1280, 5120), (1500, 1280, 1280),

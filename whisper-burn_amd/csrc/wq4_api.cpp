@@ -588,6 +588,50 @@ wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void
               ns_of(prec), static_cast<hipStream_t>(stream), dec);
 }
 
+wq4_status wq4_gemm_ln_tiled(const wq4_tensor* w, const float* bias_dev, const float* x_dev, const float* ln_w_dev,
+                             const float* ln_b_dev, void* at_scratch_dev, const float* residual_dev, float* y_dev,
+                             void* at_out_dev, int64_t rows, unsigned flags, wq4_precision prec, int kernel,
+                             void* stream) {
+  wq4_status s = check_gemm_tensor(w);
+  if (s != WQ4_OK) return s;
+  s = check_prec(prec);
+  if (s != WQ4_OK) return s;
+  if (kernel < 0 || kernel > 2) return fail(WQ4_EINVAL, "kernel must be 0, 1 or 2");
+  if (rows < 0 || rows > (1 << 24)) return fail(WQ4_ESHAPE, "bad row count");
+  if (rows == 0) return WQ4_OK;
+  if (!x_dev || !ln_w_dev || !ln_b_dev || !at_scratch_dev) return fail(WQ4_EINVAL, "null argument");
+  if (w->g.k % 4 != 0 || w->g.k > 2048) return fail(WQ4_ESHAPE, "LayerNorm width must be % 4 == 0 and <= 2048");
+  // Measured on MI355X (decode step, 32 rows, K = 1280): building the
+  // operand inside every n-tile's workgroup repeats the row statistics and
+  // the normalisation N / 32 times and ran 19.5 us against 7.8 + ~6 us for
+  // the two launches, so the fused form is opt-in (WQ4_EPI_LN_FUSED).
+  const bool dec = kernel == 0 ? use_decode(rows) : kernel == 2;
+  if ((flags & WQ4_EPI_LN_FUSED) && dec && wq4::decode_ln_supported(w->g, (int)rows)) {
+    const bool tiled_out = (flags & WQ4_EPI_TILED_OUT) != 0;
+    if (tiled_out ? !at_out_dev : !y_dev) return fail(WQ4_EINVAL, "null argument");
+    if ((flags & WQ4_EPI_RESIDUAL) && (!residual_dev || tiled_out))
+      return fail(WQ4_EINVAL, "WQ4_EPI_RESIDUAL needs a residual and an f32 output");
+    if (tiled_out && w->g.n % 32 != 0) return fail(WQ4_ESHAPE, "tiled output needs N % 32 == 0");
+    DeviceGuard dg(w->device);
+    wq4::EpiArgs epi = make_epi(bias_dev, (flags & WQ4_EPI_RESIDUAL) ? residual_dev : nullptr, y_dev, (int)w->g.n,
+                                (int)rows, (int)w->g.n, (flags & WQ4_EPI_GELU) != 0);
+    if (tiled_out) {
+      epi.out_tiled = static_cast<_Float16*>(at_out_dev);
+      epi.nbp_next = (int)((w->g.n / 32 + 1) / 2);
+    }
+    epi.lnx = x_dev;
+    epi.lng = ln_w_dev;
+    epi.lnb = ln_b_dev;
+    epi.lnd = (int)w->g.k;
+    return gemm(w, nullptr, rows, epi, tiled_out ? wq4::kEpiTiled : wq4::kEpiF32, ns_of(prec),
+                static_cast<hipStream_t>(stream), true);
+  }
+  s = wq4_layernorm(x_dev, ln_w_dev, ln_b_dev, rows, w->g.k, prec, at_scratch_dev, nullptr, stream);
+  if (s != WQ4_OK) return s;
+  return wq4_gemm_tiled(w, bias_dev, at_scratch_dev, residual_dev, y_dev, at_out_dev, rows,
+                        flags & ~WQ4_EPI_LN_FUSED, prec, kernel, stream);
+}
+
 wq4_status wq4_prepare_stream(int device, void* stream) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return fail(WQ4_EINVAL, "bad device");

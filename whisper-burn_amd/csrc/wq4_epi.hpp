@@ -17,6 +17,13 @@ struct EpiArgs {
   int n;                  // real cols
   int hm_t;               // > 0: head-major f32 output, rows grouped by hm_t (see out_index)
   int hm_d;               //      columns per part (K | V), heads of 64
+  // LayerNorm-on-load (decode kernel, LNA variants): the A operand is
+  // LayerNorm(lnx rows; lng, lnb) (layers.rs:12-32) built in registers instead
+  // of read from a pre-tiled operand.  lnx: [M][lnd] f32.
+  const float* lnx;
+  const float* lng;
+  const float* lnb;
+  int lnd;
 };
 
 // Output element index.  Row-major by default; head-major (hm_t > 0) writes

@@ -41,6 +41,9 @@ DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal);
 // wtype: kWeightsQ4 (nib/sc/colscale of wq4_layout.hpp) or kWeightsF16
 // (nib = repack_f16 fragments, sc unused, colscale = 1).
 constexpr int kWeightsQ4 = 0, kWeightsF16 = 1;
+// Whether launch_q4_gemm can build the A operand by LayerNorm-on-load
+// (EpiArgs::lnx) for this weight and row count: 8-wave decode plans.
+bool decode_ln_supported(const Q4Geom& g, int rows);
 hipError_t launch_q4_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* colscale,
                           const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int ns, const DecodeWs* ws,
                           hipStream_t st, int wtype);

@@ -29,6 +29,7 @@
 
 #include "wq4_device.hpp"
 #include "wq4_kernels.hpp"
+#include "wq4_lnmath.hpp"
 
 namespace wq4 {
 
@@ -390,7 +391,11 @@ __device__ __forceinline__ void decode_epilogue(const floatx16& s, float cs, int
   }
 }
 
-template <int NS, int EPI, int PER, int MT, int W, int WK>
+__host__ __device__ constexpr size_t decode_lds_bytes_dev(int w) {
+  return (size_t)(w == 8 ? w : w - 1) * 16 * 64 * 4 + (size_t)32 * kStageLd * 4;
+}
+
+template <int NS, int EPI, int PER, int MT, int W, int WK, bool LNA = false>
 __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* __restrict__ nib,
                                                               const uint32_t* __restrict__ sc,
                                                               const float* __restrict__ colscale,
@@ -434,24 +439,97 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
     }
   }
   // activation fragments of every m-tile, rows >= M read as zeros
-  const size_t slab = (size_t)nbp * 2 * 2 * NS * 1024;  // bytes of one m-tile (kbp = 2 nbp)
   half8 a[MT][PER][2][2][NS];
+  if constexpr (LNA) {
+    // LayerNorm on load: row statistics exactly as layernorm_kernel (one
+    // wave per row, ln_row_stats), then lane (r, hh) builds its fragments
+    // y = ((x - mean) / den) * g + b of row r, columns 32 b + 16 kk + 8 hh + j
+    // -- bit-identical to LayerNorm -> A-tiled operand -> this kernel.
+    float* lnst = reinterpret_cast<float*>(smem + decode_lds_bytes_dev(W));  // [MT * 32][2]
+    constexpr int RPW = MT * 32 / W;  // rows per wave: all their loads in flight at once
+    floatx4 v[RPW][kLnMaxV];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const __amdgpu_buffer_rsrc_t ra = brsrc(reinterpret_cast<const uint8_t*>(at) + (mt0 + mt) * slab + (size_t)bp0 * 4 * NS * 1024,
-                                            (uint32_t)cnt * 4 * NS * 1024);
-    const bool row_ok = (mt0 + mt) * 32 + r < e.m;
+    for (int q = 0; q < RPW; ++q) {
+      const int row = mt0 * 32 + wave * RPW + q;
+      const float* xr = e.lnx + (size_t)(row < e.m ? row : 0) * e.lnd;
 #pragma unroll
-    for (int i = 0; i < PER; ++i)
+      for (int i = 0; i < kLnMaxV; ++i) {
+        const int k = lane * 4 + 256 * i;
+        v[q][i] = (row < e.m && k < e.lnd) ? *reinterpret_cast<const floatx4*>(xr + k) : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
 #pragma unroll
-      for (int blk = 0; blk < 2; ++blk)
+    for (int q = 0; q < RPW; ++q) {
+      const int rr = wave * RPW + q;
+      float mean = 0.0f, den = 1.0f;
+      if (mt0 * 32 + rr < e.m) ln_row_stats(v[q], e.lnd, lane, mean, den);
+      if (lane == 0) {
+        lnst[2 * rr] = mean;
+        lnst[2 * rr + 1] = den;
+      }
+    }
+    __syncthreads();
+    const int hh = lane >> 5;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
+    for (int mt = 0; mt < MT; ++mt) {
+      const int row = (mt0 + mt) * 32 + r;
+      const bool row_ok = row < e.m;
+      const float mean = lnst[2 * (mt * 32 + r)], den = lnst[2 * (mt * 32 + r) + 1];
+      const float* xr = e.lnx + (size_t)(row_ok ? row : 0) * e.lnd;
 #pragma unroll
-          for (int q = 0; q < NS; ++q) {
-            const int frag = ((2 * i + blk) * 2 + kk) * NS + q;
-            a[mt][i][blk][kk][q] = bload_h8<0>(ra, row_ok ? frag * 1024 + lane * 16 : kOob);
+      for (int i = 0; i < PER; ++i)
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            const int k0 = (bp0 + i) * 64 + blk * 32 + kk * 16 + 8 * hh;
+            half8 hi, lo;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              hi[j] = (_Float16)0.0f;
+              lo[j] = (_Float16)0.0f;
+            }
+            if (i < cnt && row_ok && k0 < e.lnd) {
+              const floatx4 x0 = *reinterpret_cast<const floatx4*>(xr + k0);
+              const floatx4 x1 = *reinterpret_cast<const floatx4*>(xr + k0 + 4);
+              const floatx4 g0 = *reinterpret_cast<const floatx4*>(e.lng + k0);
+              const floatx4 g1 = *reinterpret_cast<const floatx4*>(e.lng + k0 + 4);
+              const floatx4 b0 = *reinterpret_cast<const floatx4*>(e.lnb + k0);
+              const floatx4 b1 = *reinterpret_cast<const floatx4*>(e.lnb + k0 + 4);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                _Float16 h0, l0, h1, l1;
+                split_f16(ln_apply(x0[j], mean, den, g0[j], b0[j]), h0, l0);
+                split_f16(ln_apply(x1[j], mean, den, g1[j], b1[j]), h1, l1);
+                hi[j] = h0;
+                lo[j] = l0;
+                hi[4 + j] = h1;
+                lo[4 + j] = l1;
+              }
+            }
+            a[mt][i][blk][kk][0] = hi;
+            if constexpr (NS == 2) a[mt][i][blk][kk][NS - 1] = lo;
           }
+    }
+  } else {
+    const size_t slab = (size_t)nbp * 2 * 2 * NS * 1024;  // bytes of one m-tile (kbp = 2 nbp)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const __amdgpu_buffer_rsrc_t ra = brsrc(reinterpret_cast<const uint8_t*>(at) + (mt0 + mt) * slab + (size_t)bp0 * 4 * NS * 1024,
+                                              (uint32_t)cnt * 4 * NS * 1024);
+      const bool row_ok = (mt0 + mt) * 32 + r < e.m;
+#pragma unroll
+      for (int i = 0; i < PER; ++i)
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int q = 0; q < NS; ++q) {
+              const int frag = ((2 * i + blk) * 2 + kk) * NS + q;
+              a[mt][i][blk][kk][q] = bload_h8<0>(ra, row_ok ? frag * 1024 + lane * 16 : kOob);
+            }
+    }
   }
 
 #pragma unroll
@@ -644,9 +722,7 @@ static size_t prefill_lds_bytes(int ns, int epi) {
   return a > s ? a : s;
 }
 
-static size_t decode_lds_bytes(int w) {
-  return (size_t)(w == 8 ? w : w - 1) * 16 * 64 * 4 + (size_t)32 * kStageLd * 4;
-}
+static size_t decode_lds_bytes(int w) { return decode_lds_bytes_dev(w) + 2 * 64 * 4; }  // + LNA row stats
 
 DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal) {
   // Smallest per-wave depth whose grid still covers ~all CUs, then balance.
@@ -730,6 +806,20 @@ static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint3
   const int mreal0 = (int)((rows + kMTile - 1) / kMTile);
   const DecodePlan p = plan_decode(g.ntiles, g.nbp, 2);
   const bool dec_ok = ws && mreal0 <= kDecodeMaxMTiles && p.per <= (p.w == 8 ? kDecodeMaxPer8 : kDecodeMaxPer);
+  if (e.lnx) {  // LayerNorm-on-load: 8-wave decode plans only (the caller falls back otherwise)
+    if (!dec_ok || p.w != 8) return hipErrorNotSupported;
+    const dim3 grid((unsigned)(g.ntiles * p.ks));
+#define WQ4_DECLN(PER_)                                                                                      \
+  hipLaunchKernelGGL((q4_gemm_decode_kernel<NS, EPI, PER_, 1, 8, WK, true>), grid, dim3(512), decode_lds_bytes(8), \
+                     st, nib, sc, cs, at, mt0, (int)g.nbp, p.ks, p.chunk, ws->part, ws->counters, e)
+    for (int mt0 = 0; mt0 < mreal0; ++mt0) {
+      if (p.per == 1) WQ4_DECLN(1);
+      else if (p.per == 2) WQ4_DECLN(2);
+      else WQ4_DECLN(3);
+    }
+#undef WQ4_DECLN
+    return hipGetLastError();
+  }
   if (dec_ok) {
     const dim3 grid((unsigned)(g.ntiles * p.ks));
 #define WQ4_DEC(PER_, MT_, W_)                                                                               \
@@ -765,6 +855,12 @@ static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint3
                        prefill_lds_bytes(NS, EPI), st, nib, sc, cs, at, mtiles, (int)g.nbp, (int)g.ntiles, e);
   }
   return hipGetLastError();
+}
+
+bool decode_ln_supported(const Q4Geom& g, int rows) {
+  const int mreal0 = (int)((rows + kMTile - 1) / kMTile);
+  const DecodePlan p = plan_decode(g.ntiles, g.nbp, 2);
+  return rows >= 1 && mreal0 <= kDecodeMaxMTiles && p.w == 8 && p.per <= kDecodeMaxPer8;
 }
 
 hipError_t launch_q4_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* colscale,

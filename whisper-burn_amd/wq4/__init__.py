@@ -89,7 +89,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.wq4_gemm_tiled_headmajor.argtypes = [vp, vp, vp, vp, c_i64, c_int, c_int, c_int, c_int, vp]
     L.wq4_layernorm.argtypes = [vp, vp, vp, c_i64, c_i64, c_int, vp, vp, vp]
     L.wq4_prepare_stream.argtypes = [c_int, vp]
-    for name in ("wq4_tile_activations", "wq4_linear_forward_tiled", "wq4_linear_forward_tiled_out", "wq4_gemm_tiled",
+    L.wq4_gemm_ln_tiled.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, c_i64, ctypes.c_uint, c_int, c_int, vp]
+    for name in ("wq4_gemm_ln_tiled", "wq4_tile_activations", "wq4_linear_forward_tiled", "wq4_linear_forward_tiled_out", "wq4_gemm_tiled",
                  "wq4_gemm_tiled_headmajor", "wq4_layernorm", "wq4_prepare_stream"):
         getattr(L, name).restype = c_int
     for name in ("wq4_device_count", "wq4_set_precision", "wq4_set_kernel_policy", "wq4_tensor_create",
