@@ -1,6 +1,7 @@
 """Summarise rocprofv3 PMC passes into profiles/pmc_traffic.json (bench.py roofline.traffic).
 
-    python scripts/pmc_summary.py ROUND   (reads gpurun_out/pmc_{FETCH_SIZE,WRITE_SIZE}_ROUND)
+    python scripts/pmc_summary.py ROUND [OUT]   (reads gpurun_out/pmc_{FETCH_SIZE,WRITE_SIZE}_ROUND,
+                                                 writes OUT, default profiles/pmc_traffic.json)
 
 HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950
 FETCH_SIZE reports half the bytes of a 16-B-per-lane streaming read and
@@ -14,7 +15,9 @@ import re
 import sys
 
 FAMILIES = {"q4_gemm_prefill_kernel": r"q4_gemm_prefill_kernel", "q4_gemm_decode_kernel": r"q4_gemm_decode_kernel",
-            "xattn_main_kernel": r"xattn_main_kernel"}
+            "xattn_main_kernel": r"xattn_main_kernel",
+            "xattn_q_kernel": r"xattn_q_kernel", "xattn_merge_kernel": r"xattn_merge_kernel",
+            "xattn_out_kernel": r"xattn_out_kernel"}
 
 
 def load(counter: str, rnd: str) -> dict:
@@ -44,8 +47,9 @@ def main() -> None:
         fk, wk = sum(f) / len(f), sum(w) / len(w)
         out["kernels"][fam] = {"launches_fetch": len(f), "launches_write": len(w), "fetch_size_kib": fk,
                                "write_size_kib": wk, "hbm_bytes_per_launch": (2 * fk + wk) * 1024}
-    os.makedirs("profiles", exist_ok=True)
-    with open("profiles/pmc_traffic.json", "w") as fh:
+    dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
+    os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
+    with open(dst, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 
