@@ -543,6 +543,155 @@ hipError_t launch_argmax_step(const float* logits, int B, int V, int min_tokens,
   return hipGetLastError();
 }
 
+// ------------------------------------------------ logits + greedy pick --
+// Decode step (B <= 32 clips): logits[b, v] = h[b] . E[v] (decoder.rs:289-292)
+// fused with the greedy argmax (whisper.rs:119-124, 131-138) -- the logits
+// never reach HBM.  Workgroup = 4 waves x 32 vocabulary rows; per 256-wide k
+// chunk the hidden rows are staged in LDS and the next chunk's embedding
+// float4s are already in flight in registers (the 265 MB f32 embedding is
+// the step's largest stream).  Each workgroup leaves one (max, index)
+// candidate per clip; the last-arriving workgroup (agent-scope ticket,
+// write-through partials: cdna_hip_programming.md Guideline 16 R1) reduces
+// them.  (value, index) is compared lexicographically -- the largest value,
+// the LARGEST index among equal maxima -- so the result equals the
+// sequential Rust max_by scan whatever the reduction order.
+constexpr int kLgChunk = 256;
+constexpr int kLgLd = kLgChunk + 4;
+
+__device__ __forceinline__ void better_pair(float& bv, int& bi, float v, int i) {
+  if (v > bv || (v == bv && i > bi)) {
+    bv = v;
+    bi = i;
+  }
+}
+
+__global__ __launch_bounds__(256) void logits_argmax_kernel(const float* __restrict__ hid, int B, int D, long ldh,
+                                                            const float* __restrict__ emb, int V, int min_tokens,
+                                                            const DecodeState* __restrict__ state,
+                                                            float* __restrict__ pval, int* __restrict__ pidx,
+                                                            int* __restrict__ counter, int* __restrict__ out_tok) {
+  __shared__ __attribute__((aligned(16))) float hs[32 * kLgLd];
+  __shared__ int ticket;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int nwg = gridDim.x;
+  const int n = blockIdx.x * 128 + wave * 32 + r;
+  const float* er = emb + (size_t)(n < V ? n : V - 1) * D;
+  const int nch = (D + kLgChunk - 1) / kLgChunk;
+  floatx16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+  floatx4 ec[kLgChunk / 8], en[kLgChunk / 8];
+  auto load_e = [&](floatx4 (&e)[kLgChunk / 8], int kc) {
+#pragma unroll
+    for (int j = 0; j < kLgChunk / 8; ++j) {
+      const int k = kc + 8 * j + 4 * h;
+      e[j] = *reinterpret_cast<const floatx4*>(er + (k < D ? k : 0));
+    }
+  };
+  load_e(ec, 0);
+  for (int c = 0; c < nch; ++c) {
+    const int kc = c * kLgChunk;
+    if (c + 1 < nch) load_e(en, kc + kLgChunk);
+    __syncthreads();
+    for (int e = tid; e < 32 * (kLgChunk / 4); e += 256) {
+      const int row = e / (kLgChunk / 4), k4 = (e % (kLgChunk / 4)) * 4;
+      const floatx4 v = (row < B && kc + k4 < D) ? *reinterpret_cast<const floatx4*>(hid + (size_t)row * ldh + kc + k4)
+                                                 : floatx4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<floatx4*>(&hs[row * kLgLd + k4]) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kLgChunk / 8; ++j) {
+      const floatx4 a = *reinterpret_cast<const floatx4*>(&hs[r * kLgLd + 8 * j + 4 * h]);
+      const bool kin = kc + 8 * j < D;  // D % 8 == 0
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = mfma_f32(kin ? a[s] : 0.0f, ec[j][s], acc);
+    }
+    if (c + 1 < nch) {
+#pragma unroll
+      for (int j = 0; j < kLgChunk / 8; ++j) ec[j] = en[j];
+    }
+  }
+  // this workgroup's 32 x 128 logits -> LDS, then (max, index) per clip
+  __syncthreads();
+  float* lg = hs;  // [32 rows][128 + 4]
+  constexpr int kLd = 132;
+  const int suppress = state->step + 1 < min_tokens;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+    float v = acc[i];
+    if (n >= V || (suppress && n == kEOT)) v = -INFINITY;
+    lg[row * kLd + wave * 32 + r] = v;
+  }
+  __syncthreads();
+  const int row = tid >> 3, part = tid & 7;
+  float bv = -INFINITY;
+  int bi = -1;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int c = part * 16 + j;
+    const int idx = blockIdx.x * 128 + c;
+    if (idx < V) better_pair(bv, bi, lg[row * kLd + c], idx);
+  }
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    const float v2 = __shfl_xor(bv, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    better_pair(bv, bi, v2, i2);
+  }
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(pval, 0, 32 * nwg * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(pidx, 0, 32 * nwg * 4, 0x00020000);
+  if (part == 0 && row < B) {
+    const uint32_t off = (uint32_t)(row * nwg + blockIdx.x) * 4;
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bv), rv, off, 0, 16);  // sc1
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)bi, ri, off, 0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    typedef __attribute__((address_space(1))) int gint;
+    const int prev = __hip_atomic_fetch_add((gint*)counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = prev == nwg - 1;
+  }
+  __syncthreads();
+  if (!ticket) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: loads stay below the ticket
+  bv = -INFINITY;
+  bi = -1;
+  if (row < B) {
+    for (int j = part; j < nwg; j += 8) {
+      const uint32_t off = (uint32_t)(row * nwg + j) * 4;
+      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, off, 0, 16));
+      const int i = (int)__builtin_amdgcn_raw_buffer_load_b32(ri, off, 0, 16);
+      better_pair(bv, bi, v, i);
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    const float v2 = __shfl_xor(bv, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    better_pair(bv, bi, v2, i2);
+  }
+  if (part == 0 && row < B) out_tok[row] = bi < 0 ? 0 : bi;
+  if (tid == 0) {
+    typedef __attribute__((address_space(1))) int gint;
+    __hip_atomic_store((gint*)counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  }
+}
+
+int logits_argmax_groups(int V) { return (V + 127) / 128; }
+
+hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const float* emb, int V, int min_tokens,
+                                const DecodeState* state, float* pval, int* pidx, int* counter, int* out_tok,
+                                hipStream_t st) {
+  if (B < 1 || B > 32 || D % 8 != 0 || !state) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(logits_argmax_kernel, dim3(logits_argmax_groups(V)), dim3(256), 0, st, h, B, D, ldh, emb, V,
+                     min_tokens, state, pval, pidx, counter, out_tok);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------ bookkeep --
 __global__ void bookkeep_kernel(const int* __restrict__ next, int* __restrict__ tokens, int* __restrict__ ntok,
                                 int* __restrict__ done, int B, int max_tokens, int eot_stop, DecodeState* state) {

@@ -76,6 +76,15 @@ hipError_t launch_logits(const float* h, int B, int D, long ldh, const float* em
 hipError_t launch_argmax(const float* logits, int B, int V, int lo, int hi, int suppress_eot,
                          const DecodeState* state, int* out_tok, int out_stride, hipStream_t st);
 
+// Decode-step logits fused with the greedy pick (launch_logits +
+// launch_argmax_step in one kernel, logits never stored): B <= 32 rows,
+// D % 8 == 0; pval / pidx: 32 * logits_argmax_groups(V) scratch each,
+// counter: one int zeroed once (re-armed by the kernel).
+int logits_argmax_groups(int V);
+hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const float* emb, int V, int min_tokens,
+                                const DecodeState* state, float* pval, int* pidx, int* counter, int* out_tok,
+                                hipStream_t st);
+
 // Greedy-loop bookkeeping at the top of each step (whisper.rs:104-115):
 // for every clip not yet done, EOT -> done (eot_stop != 0), else append the
 // next token; then advance position / kv_len / step.

@@ -168,6 +168,8 @@ struct DecGroup {
   int *prompt_tok, *next_tok, *tokens, *ntok, *done;
   _Float16* xqt;    // cross-attention Wk^T q operands [rows][ns][16*ceil(H/16)][D]
   float* xattn_part;  // cross-attention split partials (Z, max, sum)
+  float* lg_val;      // fused logits + argmax: per-workgroup candidates [32][groups]
+  int *lg_idx, *lg_ctr;
   wa::DecodeState* state;
   int* host_ndone = nullptr;  // pinned ring
   hipGraphExec_t graph = nullptr;
@@ -563,11 +565,16 @@ wq4_status alloc_activations(wa_model* m) {
     g.state = d.alloc<wa::DecodeState>(1);
     g.xattn_part = f32((int64_t)xpart);
     g.xqt = d.alloc<_Float16>((size_t)rdec * m->ns * HP * Dt);
+    g.lg_val = f32((int64_t)32 * wa::logits_argmax_groups(c.n_vocab));
+    g.lg_idx = d.alloc<int>((size_t)32 * wa::logits_argmax_groups(c.n_vocab));
+    g.lg_ctr = d.alloc<int>(1);
     m->bytes += (size_t)rdec * m->ns * HP * Dt * 2;
     for (void* p : {(void*)g.xd, (void*)g.qkvd, (void*)g.qd, (void*)g.hid, (void*)g.logits, (void*)g.atd_dec,
                     (void*)g.atf_dec, (void*)g.prompt_tok, (void*)g.next_tok, (void*)g.tokens, (void*)g.ntok,
-                    (void*)g.done, (void*)g.state, (void*)g.xattn_part, (void*)g.xqt})
+                    (void*)g.done, (void*)g.state, (void*)g.xattn_part, (void*)g.xqt, (void*)g.lg_val,
+                    (void*)g.lg_idx, (void*)g.lg_ctr})
       if (!p) return fail(WQ4_ENOMEM, "decode-group allocation failed");
+    WA_HIP(hipMemset(g.lg_ctr, 0, sizeof(int)));
     WA_HIP(hipMemset(g.xqt, 0, (size_t)rdec * m->ns * HP * Dt * 2));  // padded heads stay 0
     WA_HIP(hipMemset(g.atd_dec, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
     WA_HIP(hipMemset(g.atf_dec, 0, wq4_atiled_bytes(rdec, Ft, m->prec)));
@@ -682,6 +689,13 @@ wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st) {
   return WQ4_OK;
 }
 
+// A greedy decode step of <= 32 clips picks its tokens inside the logits
+// kernel (wa::launch_logits_argmax); prompts and larger groups keep the
+// stored logits + separate argmax.
+bool fused_pick(const DecGroup& g, int Tq, const wa::DecodeState* state) {
+  return state != nullptr && Tq == 1 && g.nb <= 32;
+}
+
 // Decoder pass over Tq new tokens for the clips of group g (forward_prompt
 // when state == nullptr, decode_step otherwise), ending in last-position
 // logits.  Self-KV and cross-K/V are addressed at the group's clip offset.
@@ -713,6 +727,11 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
   // final LN (decoder.rs:286 / 340) and tied-embedding logits of the last
   // position of every clip (decoder.rs:289-292, 342-343)
   WA_WQ4(wq4_layernorm(g.xd, m->dln_w, m->dln_b, rows, D, WQ4_PREC_F16X2, nullptr, g.hid, st));
+  if (fused_pick(g, Tq, state)) {  // decode step: logits + greedy pick in one kernel, into next_tok
+    WA_HIP(wa::launch_logits_argmax(g.hid, B, D, D, m->tok_emb, c.n_vocab, kMinTokens, state, g.lg_val, g.lg_idx,
+                                    g.lg_ctr, g.next_tok, st));
+    return WQ4_OK;
+  }
   WA_HIP(wa::launch_logits(g.hid + (size_t)(Tq - 1) * D, B, D, (int64_t)Tq * D, m->tok_emb, c.n_vocab, g.logits,
                            st));
   return WQ4_OK;
@@ -723,7 +742,8 @@ wq4_status decode_step(wa_model* m, DecGroup& g, int eot_stop, hipStream_t st) {
   WA_HIP(wa::launch_bookkeep(g.next_tok, g.tokens, g.ntok, g.done, g.nb, kMaxTokens, eot_stop, g.state, st));
   wq4_status s = decoder_forward(m, g, g.next_tok, 1, g.state, 0, 0, st);
   if (s != WQ4_OK) return s;
-  WA_HIP(wa::launch_argmax_step(g.logits, g.nb, m->cfg.n_vocab, kMinTokens, g.state, g.next_tok, st));
+  if (!fused_pick(g, 1, g.state))
+    WA_HIP(wa::launch_argmax_step(g.logits, g.nb, m->cfg.n_vocab, kMinTokens, g.state, g.next_tok, st));
   return WQ4_OK;
 }
 
