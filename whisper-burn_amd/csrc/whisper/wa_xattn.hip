@@ -38,11 +38,12 @@ using wq4::kbp_of;
 using wq4::split_f16;
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWtQ4 = 0, kWtF16 = 1;  // raw weight formats (wa_model wtype)
 constexpr int kTc = 16;          // keys (encoder frames) per sub-chunk
 constexpr int kMaxD = 1280;
-constexpr int kMaxSplits = 8;  // xattn_out_kernel keeps a column's split values in registers
+constexpr int kMaxSplits = 16;  // frame ranges per query row (merge weights in xattn_out_kernel LDS)
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -391,41 +392,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   }
 }
 
-// ------------------------------------------------------ merge the splits --
-// grid (ceil(D / 256), H, R), 256 threads: Zn[r][h][c] = sum_s w_s Z_s[c],
-// w_s = exp(M_s - max) / sum_s' exp(M_s' - max) L_s' (the flash-attention
-// merge of the S frame ranges), for 256 columns per workgroup: the partial
-// stream is spread over many workgroups.
-__global__ __launch_bounds__(256) void xattn_merge_kernel(const float* __restrict__ zpart,
-                                                          const float* __restrict__ mlpart, int R, int H, int D,
-                                                          int S, float* __restrict__ zn) {
-  const int h = blockIdx.y, r = blockIdx.z, c = blockIdx.x * 256 + threadIdx.x;
-  float m[kMaxSplits], lv[kMaxSplits], zv[kMaxSplits];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int s = 0; s < kMaxSplits; ++s) {
-    m[s] = -INFINITY;
-    lv[s] = 0.0f;
-    zv[s] = 0.0f;
-    if (s < S) {
-      const size_t b = ((size_t)r * S + s) * H + h;
-      m[s] = mlpart[b * 2];
-      lv[s] = mlpart[b * 2 + 1];
-      if (c < D) zv[s] = zpart[b * D + c];
-    }
-    mx = fmaxf(mx, m[s]);
-  }
-  float lsum = 0.0f, acc = 0.0f;
-#pragma unroll
-  for (int s = 0; s < kMaxSplits; ++s) {
-    const float a = m[s] == -INFINITY ? 0.0f : expf(m[s] - mx);
-    lsum = fmaf(a, lv[s], lsum);
-    acc = fmaf(a, zv[s], acc);
-  }
-  if (c < D) zn[((size_t)r * H + h) * D + c] = acc / lsum;
-}
-
-// ------------------------------------------------------- out = Wv Zn + bv --
+// ---------------------------------------- merge + out = Wv Zn + bv --
 // grid (H, ceil(R / 4)), 512 threads: the head's 64 raw Wv rows (46 KB of
 // Q4_0 blocks) and 4 rows of Zn ([column] x 4 rows) in LDS; thread (row pair
 // d, d + 32; blocks b, b + 16, b + 32) dequantizes each block once for the 4
@@ -433,7 +400,8 @@ __global__ __launch_bounds__(256) void xattn_merge_kernel(const float* __restric
 // out[r][h*64 + d] + bv goes into the A-tiled operand of the output
 // projection.
 template <int NS, int WK>
-__global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict__ zn, int R, int H, int D,
+__global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict__ zpart,
+                                                        const float* __restrict__ mlpart, int R, int H, int D, int S,
                                                         const uint8_t* __restrict__ wv,
                                                         const float* __restrict__ bv, _Float16* __restrict__ tiled) {
   constexpr int kStage = WK == kWtQ4 ? 64 * (kMaxD / 32) * 18 : 16;  // 46 KB of Q4 blocks
@@ -443,18 +411,56 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
   const int h = blockIdx.x, r0 = blockIdx.y * 4, tid = threadIdx.x;
   const int nkb = D / 32;
   const size_t rowbytes = (size_t)nkb * 18;
-  if (WK == kWtQ4) {  // the head's 64 rows are contiguous: 64 * nkb * 18 bytes in 16-B chunks
+  if (WK == kWtQ4) {  // the head's 64 rows are contiguous: 64 * nkb * 18 bytes
     const uint8_t* src = wv + (size_t)h * 64 * rowbytes;
-    const int n16 = (int)(64 * rowbytes / 16);
-    for (int i = tid; i < n16; i += 512)
-      *reinterpret_cast<uint4*>(&sw[i * 16]) = *reinterpret_cast<const uint4*>(src + (size_t)i * 16);
+    // LDS-DMA (global_load_lds_dwordx4): 1 KiB pieces straight into the
+    // stage, every piece of a wave in flight at once (64 * 720 B = 45 KiB)
+    const int nbytes = (int)(64 * rowbytes);  // a multiple of 16 (64 * 18 * D / 32)
+    const int w = tid >> 6, lane = tid & 63;
+    for (int pc = w; pc * 1024 < nbytes; pc += 8)
+      if (pc * 1024 + lane * 16 < nbytes) wq4::glds16(src + (size_t)pc * 1024 + lane * 16, &sw[pc * 1024]);
   }
-  for (int c = tid; c < D; c += 512) {
-    floatx4 v;
+  // merge of the S frame ranges (flash-attention merge, fixed split order):
+  // Zn[c] = (sum_s w_s Z_s[c]) / (sum_s w_s L_s), w_s = exp(M_s - max_s M_s).
+  // Item (row j, 4 columns): the row's (M_s, L_s) and every split's float4
+  // are loaded together (fixed unrolled count; splits >= S read nothing), so
+  // the merge costs one memory round trip; rows >= R give zeros.
+  {
+    const int nq = D / 4;
+    float* zsf = reinterpret_cast<float*>(zs);
+    for (int it = tid; it < 4 * nq; it += 512) {
+      const int j = it / nq, q = it - j * nq;
+      const bool rok = r0 + j < R;
+      const size_t rb = (size_t)(rok ? r0 + j : 0) * S;
+      const floatx4* zp = reinterpret_cast<const floatx4*>(zpart + (rb * H + h) * D) + q;
+      const floatx2* mp = reinterpret_cast<const floatx2*>(mlpart) + rb * H + h;
+      floatx4 zv[kMaxSplits];
+      floatx2 ml[kMaxSplits];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = r0 + j < R ? zn[((size_t)(r0 + j) * H + h) * D + c] : 0.0f;
-    zs[c] = v;
+      for (int s = 0; s < kMaxSplits; ++s)
+        if (s < S) {
+          ml[s] = mp[(size_t)s * H];
+          zv[s] = zp[(size_t)s * H * (D / 4)];
+        }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int s = 0; s < kMaxSplits; ++s)
+        if (s < S) mx = fmaxf(mx, ml[s][0]);
+      float lsum = 0.0f;
+      floatx4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s = 0; s < kMaxSplits; ++s)
+        if (s < S) {
+          const float w = ml[s][0] == -INFINITY ? 0.0f : expf(ml[s][0] - mx);
+          lsum = fmaf(w, ml[s][1], lsum);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[e] = fmaf(w, zv[s][e], acc[e]);
+        }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) zsf[(4 * q + e) * 4 + j] = rok ? acc[e] / lsum : 0.0f;
+    }
   }
+  if (WK == kWtQ4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stage pieces landed
   __syncthreads();
   const int dp = tid & 31, bg = tid >> 5;  // rows dp, dp + 32; blocks bg, bg + 16, bg + 32
   floatx4 acc0{0.0f, 0.0f, 0.0f, 0.0f}, acc1{0.0f, 0.0f, 0.0f, 0.0f};
@@ -639,21 +645,18 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   WA_XMAIN(384, 1)
   return hipErrorInvalidValue;
 #undef WA_XMAIN
-  // merge the splits, then project with Wv into the output projection's operand
-  float* zn = ml + (size_t)R * p.splits * H * 2;
-  hipLaunchKernelGGL(xattn_merge_kernel, dim3((D + 255) / 256, H, R), dim3(256), 0, st, z, ml, R, H, D, p.splits,
-                     zn);
+  // merge the splits and project with Wv into the output projection's operand
   const dim3 go(H, (R + 3) / 4);
   if (wtype == kWtQ4) {
     if (ns == 2)
-      hipLaunchKernelGGL((xattn_out_kernel<2, kWtQ4>), go, dim3(512), 0, st, zn, R, H, D, wv, bv, tiled);
+      hipLaunchKernelGGL((xattn_out_kernel<2, kWtQ4>), go, dim3(512), 0, st, z, ml, R, H, D, p.splits, wv, bv, tiled);
     else
-      hipLaunchKernelGGL((xattn_out_kernel<1, kWtQ4>), go, dim3(512), 0, st, zn, R, H, D, wv, bv, tiled);
+      hipLaunchKernelGGL((xattn_out_kernel<1, kWtQ4>), go, dim3(512), 0, st, z, ml, R, H, D, p.splits, wv, bv, tiled);
   } else {
     if (ns == 2)
-      hipLaunchKernelGGL((xattn_out_kernel<2, kWtF16>), go, dim3(512), 0, st, zn, R, H, D, wv, bv, tiled);
+      hipLaunchKernelGGL((xattn_out_kernel<2, kWtF16>), go, dim3(512), 0, st, z, ml, R, H, D, p.splits, wv, bv, tiled);
     else
-      hipLaunchKernelGGL((xattn_out_kernel<1, kWtF16>), go, dim3(512), 0, st, zn, R, H, D, wv, bv, tiled);
+      hipLaunchKernelGGL((xattn_out_kernel<1, kWtF16>), go, dim3(512), 0, st, z, ml, R, H, D, p.splits, wv, bv, tiled);
   }
   return hipGetLastError();
 }
