@@ -238,8 +238,8 @@ def main() -> None:
         xa_gbs = xa["bytes"] / (xa["us"] * 1e-6) * 1e-9
         roof_xa = {"bound": "hbm", "achieved": round(xa_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                    "frac": round(xa_gbs / PEAK_HBM_GBS, 4), "traffic": pmc_traffic("xattn_main_kernel"),
-                   "kernel": "cross-attention over the encoder output: xattn_q + xattn_main + xattn_out (split merge fused) + "
-                             "xattn_out (decode step, Tq = 1)", "avg_us": round(xa["us"], 2),
+                   "kernel": "cross-attention over the encoder output: xattn_q + xattn_main + xattn_out "
+                             "(split merge fused; decode step, Tq = 1)", "avg_us": round(xa["us"], 2),
                    "bytes_per_launch": xa["bytes"],
                    "total_ms_per_step": round(xa["us"] * 1e-3 * cfg["n_text_layer"] * steps_run, 2)}
         dq = probe["decode_fc1"]
