@@ -410,6 +410,9 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
   __shared__ float red[16][64][5];
   const int h = blockIdx.x, r0 = blockIdx.y * 4, tid = threadIdx.x;
   const int nkb = D / 32;
+  // the value bias of this thread's final outputs, loaded up front
+  const floatx4 bias4 = tid < 64 ? *reinterpret_cast<const floatx4*>(bv + h * 64 + 4 * (tid & 15))
+                                 : floatx4{0.f, 0.f, 0.f, 0.f};
   const size_t rowbytes = (size_t)nkb * 18;
   if (WK == kWtQ4) {  // the head's 64 rows are contiguous: 64 * nkb * 18 bytes
     const uint8_t* src = wv + (size_t)h * 64 * rowbytes;
@@ -517,7 +520,7 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
       float o[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float sacc = bv[h * 64 + d0 + i];
+        float sacc = bias4[i];
 #pragma unroll
         for (int g = 0; g < 16; ++g) sacc += red[g][d0 + i][j];
         o[i] = sacc;
@@ -561,9 +564,19 @@ __global__ __launch_bounds__(256) void untile_kernel(const _Float16* __restrict_
 template <int D, int HT, int NS>
 void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T, int H, int S, int CH, float* z,
                  float* ml, hipStream_t st) {
-  constexpr int NW = (D / 8) % 32 == 0 ? 8 : 4, PF = 1;
-  hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, NW, PF>), g, dim3(64 * NW), 0, st, qt, enc, Tq, T, H, S, CH, z,
-                     ml);
+  static const int variant = [] {  // tuning knob: 0 = 8 waves / 1 sub-chunk in flight, 1 = 4 waves / 2
+    const char* e = getenv("WA_XATTN_MAIN");
+    return e ? atoi(e) : 0;
+  }();
+  if constexpr ((D / 8) % 32 == 0) {
+    if (variant == 1) {
+      hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 4, 2>), g, dim3(256), 0, st, qt, enc, Tq, T, H, S, CH, z, ml);
+      return;
+    }
+    hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z, ml);
+  } else {
+    hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 4, 1>), g, dim3(256), 0, st, qt, enc, Tq, T, H, S, CH, z, ml);
+  }
 }
 
 }  // namespace

@@ -31,6 +31,16 @@ __device__ __forceinline__ float epi_value(float acc, int row, int col, const Ep
   return v;
 }
 
+// epi_value with bias[col] / residual[row][col] already loaded (same
+// arithmetic, same order).
+__device__ __forceinline__ float epi_value_pre(float acc, float bias, float res, const EpiArgs& e) {
+  float v = acc;
+  if (e.bias) v = v + bias;
+  if (e.gelu) v = gelu_tanh(v);
+  if (e.residual) v = res + v;
+  return v;
+}
+
 // One repacked u32 (8 nibbles, see wq4_layout.hpp) -> 8 exact f16 (q - 8),
 // element order j = 0..7:
 //   (w & 0x000F000F) | 0x64006400 = f16 pair (1024 + q_a, 1024 + q_b)

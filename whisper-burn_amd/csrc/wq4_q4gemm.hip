@@ -416,6 +416,20 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
   const int bp0 = min(nbp, (slice * W + wave) * chunk);  // chunk <= PER (launcher)
   const int cnt = max(0, min(nbp, bp0 + chunk) - bp0);
   const float cs = colscale[nt * 32 + r];
+  // 8-wave plans: the epilogue operands of this lane's two outputs (rows
+  // acc_row(2 wave + q, h), column nt * 32 + r) are loaded up front so they
+  // are not a memory round trip after the MFMAs (bias, residual: never
+  // written by this launch before its own epilogue reads them).
+  float pre_bias = 0.0f, pre_res[2] = {0.0f, 0.0f};
+  if constexpr (W == 8 && EPI != kEpiHeadMajor) {
+    const int col = nt * 32 + r;
+    if (e.bias && col < e.n) pre_bias = e.bias[col];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int row = mt0 * 32 + acc_row(2 * wave + q, lane >> 5);
+      if (e.residual && row < e.m && col < e.n) pre_res[q] = e.residual[(size_t)row * e.ldo + col];
+    }
+  }
 
   // this wave's weights (once-read stream: nt) -- zeros past cnt
   const size_t t0 = (size_t)nt * nbp + bp0;
@@ -625,11 +639,13 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
         const int rl = acc_row(i, h);
         const int row = (mt0 + mt) * 32 + rl;
         if constexpr (EPI == kEpiTiled) {
-          stage[rl * kStageLd + r] = (row < e.m && col < e.n) ? epi_value(v[q] * cs, row, col, e) : 0.0f;
+          stage[rl * kStageLd + r] =
+              (row < e.m && col < e.n) ? epi_value_pre(v[q] * cs, pre_bias, pre_res[q], e) : 0.0f;
+        } else if constexpr (EPI == kEpiHeadMajor) {
+          if (row < e.m && col < e.n) e.out[out_index(e, row, col)] = epi_value(v[q] * cs, row, col, e);
         } else {
           if (row < e.m && col < e.n)
-            e.out[EPI == kEpiHeadMajor ? out_index(e, row, col) : (size_t)row * e.ldo + col] =
-                epi_value(v[q] * cs, row, col, e);
+            e.out[(size_t)row * e.ldo + col] = epi_value_pre(v[q] * cs, pre_bias, pre_res[q], e);
         }
       }
       if constexpr (EPI == kEpiTiled) {
