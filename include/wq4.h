@@ -178,6 +178,42 @@ wq4_status wq4_gemm_ln_tiled(const wq4_tensor* w, const float* bias_dev, const f
                              void* at_out_dev, int64_t rows, unsigned flags, wq4_precision prec, int kernel,
                              void* stream);
 
+/* LayerNorm folded into the decoder GEMMs around it (decode-sized rows,
+ * the 8-wave decode plans; replaces the wq4_layernorm launch between a
+ * residual GEMM and the GEMM that reads LayerNorm of its output -- the
+ * attn_ln / cross_attn_ln / mlp_ln -> Q4Linear pairs of decoder.rs:77-112).
+ * LN(x) = (x - mean) / sqrt(var + 1e-5) * gamma + beta (layers.rs:12-32), so
+ *   W LN(x) + bias = (W (x * gamma) - mean * (W gamma)) / sqrt(var + 1e-5)
+ *                    + (W beta + bias).
+ * Producer (set gamma_dev, at_out_dev, stats_out_dev): a residual GEMM
+ * (WQ4_EPI_RESIDUAL, f32 output x) also writes the A-tiled operand of
+ * x * gamma (wq4_atiled_bytes(rows, N, prec)) and, per (row, 32-column
+ * tile), the tile mean and sum of squared deviations (stats_out_dev,
+ * rows * N/32 * 2 floats).  Consumer (set stats_in_dev, wg_dev): at_dev is
+ * that operand; the row statistics are merged (Chan et al., fixed order)
+ * and the correction applied before bias / GELU / tiled output; bias_dev is
+ * W beta + bias and wg_dev W gamma (wq4_ln_fold_vectors).  A launch may be
+ * both.  Not bit-identical to wq4_layernorm -> wq4_gemm_tiled (re-associated
+ * sums; tolerance in tests/test_q4_gpu.py). */
+typedef struct wq4_ln_fold {
+  const float* gamma_dev;     /* producer: gamma of the LayerNorm that follows */
+  void* at_out_dev;           /* producer: A-tiled x * gamma */
+  float* stats_out_dev;       /* producer: [rows][N/32][2] */
+  const float* stats_in_dev;  /* consumer: the producer's statistics (K/32 tiles) */
+  const float* wg_dev;        /* consumer: W gamma [N] */
+} wq4_ln_fold;
+wq4_status wq4_gemm_tiled_lnfold(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
+                                 const float* residual_dev, float* y_dev, void* at_out_dev, int64_t rows,
+                                 unsigned flags, wq4_precision prec, const wq4_ln_fold* fold, void* stream);
+/* Host: wg = W gamma and bias_out = W beta + bias (bias may be NULL) for a
+ * consumer of wq4_gemm_tiled_lnfold, accumulated in double from the
+ * dequantized weights.  gamma / beta: K floats; outputs N floats. */
+wq4_status wq4_ln_fold_vectors(const wq4_tensor* w, const float* gamma, const float* beta, const float* bias,
+                               float* wg_out, float* bias_out);
+/* Whether wq4_gemm_tiled_lnfold supports w at this row count (a consumer
+ * also needs K % 32 == 0 and K <= 2048). */
+int wq4_lnfold_supported(const wq4_tensor* w, int64_t rows);
+
 /* Allocate (once) the per-(device, stream) split-K workspace that small-M
  * GEMMs on `stream` use.  The first small-M GEMM on a stream does this
  * itself, which is not allowed inside a graph capture: call this first when

@@ -453,3 +453,91 @@ def test_f16_weights_batch_invariance(torch):
     yb = wq4.q4_matmul(xb, t).cpu().numpy()
     y1 = wq4.q4_matmul(xb[5:6].contiguous(), t).cpu().numpy()
     assert np.array_equal(yb[5:6].view(np.uint32), y1.view(np.uint32))
+
+
+# ------------------------------ LayerNorm folded into the decoder GEMMs --
+@pytest.mark.parametrize("wtype", ["q4_0", "f16"])
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("m", [1, 7, 32, 100])
+@pytest.mark.parametrize("n2,flags", [(1280, 0), (5120, 1)])
+def test_ln_fold_matches_layernorm_path(torch, wtype, prec, m, n2, flags):
+    """wq4_gemm_tiled_lnfold: a residual GEMM x = r + W1 a + b1 that also
+    emits tiled(x * gamma) and tile statistics (producer), then a GEMM on
+    LayerNorm(x) (consumer, decoder.rs:77-112 attn_ln -> query etc.),
+    against wq4_gemm_tiled -> wq4_layernorm -> wq4_gemm_tiled.  The
+    producer's x is bit-identical; the consumer re-associates
+    W LN(x) = (W (x gamma) - mean W gamma) / den + W beta, so it is held to
+    |z - z_ref| <= 2e-5 * (1 + max|z_ref|) (f32 reference arithmetic itself
+    is ~1e-6 here)."""
+    import ctypes
+
+    d = 1280
+    rng = np.random.default_rng(m * 13 + n2 + prec)
+
+    def weights(n, k, s):
+        if wtype == "f16":
+            return wq4.Q4Tensor.from_f16((rng.standard_normal((n, k)) * s).astype(np.float16))
+        return wq4.Q4Tensor.from_q4_bytes(oracle.quantize_convert_np((rng.standard_normal(n * k) * s).astype(np.float32)),
+                                          [n, k])
+
+    w1, w2 = weights(d, d, 0.05), weights(n2, d, 0.04)
+    a = to_dev(torch, rng.standard_normal(m * d).astype(np.float32), (m, d))
+    res = to_dev(torch, (rng.standard_normal(m * d) * 2 + 0.7).astype(np.float32), (m, d))
+    b1 = to_dev(torch, (rng.standard_normal(d) * 0.1).astype(np.float32), (d,))
+    b2 = rng.standard_normal(n2).astype(np.float32) * 0.1
+    g = rng.uniform(0.8, 1.2, d).astype(np.float32)
+    be = rng.uniform(-0.1, 0.1, d).astype(np.float32)
+    L = wq4.lib()
+    assert L.wq4_lnfold_supported(w1.handle, m) == 1 and L.wq4_lnfold_supported(w2.handle, m) == 1
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    fp = lambda v: v.ctypes.data_as(ctypes.POINTER(ctypes.c_float))  # noqa: E731
+    at_a = torch.zeros(L.wq4_atiled_bytes(m, d, prec), dtype=torch.uint8, device="cuda:0")
+    wq4.check(L.wq4_tile_activations(p(a), m, d, d, prec, p(at_a), at_a.numel(), st))
+    tiled = (flags & 4) != 0
+    gd, bed, b2d = (to_dev(torch, v, v.shape) for v in (g, be, b2))
+
+    # reference: residual GEMM, LayerNorm kernel, GEMM
+    x_ref = res.clone()
+    wq4.check(L.wq4_gemm_tiled(w1.handle, p(b1), p(at_a), p(x_ref), p(x_ref), None, m, 2, prec, 2, st))
+    at_ln = torch.zeros(L.wq4_atiled_bytes(m, d, prec), dtype=torch.uint8, device="cuda:0")
+    wq4.check(L.wq4_layernorm(p(x_ref), p(gd), p(bed), m, d, prec, p(at_ln), None, st))
+    ob = L.wq4_atiled_bytes(m, n2, prec)
+    z_ref = torch.zeros((m, n2), device="cuda:0")
+    zt_ref = torch.zeros(ob, dtype=torch.uint8, device="cuda:0")
+    wq4.check(L.wq4_gemm_tiled(w2.handle, p(b2d), p(at_ln), None, None if tiled else p(z_ref), p(zt_ref) if tiled else None,
+                               m, flags, prec, 2, st))
+
+    # fold: producer then consumer
+    wg = np.zeros(n2, np.float32)
+    b2f = np.zeros(n2, np.float32)
+    wq4.check(L.wq4_ln_fold_vectors(w2.handle, fp(g), fp(be), fp(b2), fp(wg), fp(b2f)))
+    wgd, b2fd = to_dev(torch, wg, wg.shape), to_dev(torch, b2f, b2f.shape)
+    x = res.clone()
+    at_f = torch.zeros(L.wq4_atiled_bytes(m, d, prec), dtype=torch.uint8, device="cuda:0")
+    stats = torch.zeros(m * (d // 32) * 2, device="cuda:0")
+    prod = wq4.LnFold(gd.data_ptr(), at_f.data_ptr(), stats.data_ptr(), None, None)
+    wq4.check(L.wq4_gemm_tiled_lnfold(w1.handle, p(b1), p(at_a), p(x), p(x), None, m, 2, prec, ctypes.byref(prod), st))
+    cons = wq4.LnFold(None, None, None, stats.data_ptr(), wgd.data_ptr())
+    z = torch.zeros((m, n2), device="cuda:0")
+    zt = torch.zeros(ob, dtype=torch.uint8, device="cuda:0")
+    wq4.check(L.wq4_gemm_tiled_lnfold(w2.handle, p(b2fd), p(at_f), None, None if tiled else p(z), p(zt) if tiled else None,
+                                      m, flags, prec, ctypes.byref(cons), st))
+    torch.cuda.synchronize()
+    assert np.array_equal(x.cpu().numpy().view(np.uint32), x_ref.cpu().numpy().view(np.uint32))
+    # both paths against float64 arithmetic on the same x, held to the Q4
+    # GEMM tolerance of this file (per output: c * sum_k |W[n,k] LN(x)[k]|,
+    # c = 8e-6 f16x2 / 1.2e-3 f16 -- twice test_q4_linear's, as the fold
+    # rounds x * gamma instead of LN(x))
+    xs = x_ref.cpu().numpy().astype(np.float64)
+    mu = xs.mean(axis=1, keepdims=True)
+    ln = (xs - mu) / np.sqrt(((xs - mu) ** 2).mean(axis=1, keepdims=True) + 1e-5) * g + be
+    w2d = w2.dequantize_host().astype(np.float64)
+    z64 = ln @ w2d.T + b2
+    if flags & 1:
+        z64 = 0.5 * z64 * (1.0 + np.tanh(0.7978845608028654 * (z64 + 0.044715 * z64 ** 3)))
+    scale = np.abs(ln) @ np.abs(w2d).T
+    c = 8e-6 if prec == 0 else 1.2e-3
+    for zz in (z_ref, z):
+        err = np.abs(zz.cpu().numpy() - z64)
+        assert np.all(err <= c * scale + 1e-6), float(np.max(err / (scale + 1e-30)))

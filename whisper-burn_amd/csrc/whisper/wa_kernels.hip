@@ -443,6 +443,63 @@ hipError_t launch_embed(const int* tokens, const float* tok_emb, const float* po
   return hipGetLastError();
 }
 
+// Embedding + the LayerNorm-fold producer of the first decoder layer's
+// attn_ln (wq4_gemm_tiled_lnfold): x rows as embed_kernel, plus the A-tiled
+// operand of x * gamma and per (row, 32-column tile) the tile mean and sum
+// of squared deviations.  One workgroup per row; thread t owns the float4 at
+// columns 4 t + 1024 i, so a tile is 8 consecutive lanes.
+template <int NS>
+__global__ __launch_bounds__(256) void embed_fold_kernel(const int* __restrict__ tokens, const float* __restrict__ te,
+                                                         const float* __restrict__ pe, int Tq, int D,
+                                                         const DecodeState* state, int pos0, float* __restrict__ x,
+                                                         const float* __restrict__ gamma, _Float16* __restrict__ at,
+                                                         float* __restrict__ stats) {
+  const int row = blockIdx.x;  // b * Tq + t
+  const int t = row % Tq;
+  const int p = (state ? state->position : pos0) + t;
+  const int tok = tokens[row];
+  const int kbp = kbp_of(D);
+  for (int c = 4 * threadIdx.x; c < ((D + 1023) / 1024) * 1024; c += 1024) {
+    const bool in = c < D;  // D % 32 == 0: a tile is wholly in or out
+    floatx4 v = {0.f, 0.f, 0.f, 0.f}, g = {0.f, 0.f, 0.f, 0.f};
+    if (in) {
+      const floatx4 a = *reinterpret_cast<const floatx4*>(te + (size_t)tok * D + c);
+      const floatx4 b = *reinterpret_cast<const floatx4*>(pe + (size_t)p * D + c);
+      g = *reinterpret_cast<const floatx4*>(gamma + c);
+      v = a + b;
+      *reinterpret_cast<floatx4*>(x + (size_t)row * D + c) = v;
+      atile_store4<NS>(at, row, c, kbp, v[0] * g[0], v[1] * g[1], v[2] * g[2], v[3] * g[3]);
+    }
+    float sum = (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) sum += __shfl_xor(sum, o, 64);
+    const float mean = sum * (1.0f / 32.0f);
+    float m2 = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m2 += (v[j] - mean) * (v[j] - mean);
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) m2 += __shfl_xor(m2, o, 64);
+    if (in && (threadIdx.x & 7) == 0) {
+      float* st = stats + ((size_t)row * (D / 32) + c / 32) * 2;
+      st[0] = mean;
+      st[1] = m2;
+    }
+  }
+}
+
+hipError_t launch_embed_fold(const int* tokens, const float* tok_emb, const float* pos_emb, int B, int Tq, int D,
+                             const DecodeState* state, int pos0_host, float* x, const float* gamma, _Float16* at,
+                             float* stats, int ns, hipStream_t st) {
+  if (D % 32 != 0) return hipErrorInvalidValue;
+  if (ns == 2)
+    hipLaunchKernelGGL(embed_fold_kernel<2>, dim3(B * Tq), dim3(256), 0, st, tokens, tok_emb, pos_emb, Tq, D, state,
+                       pos0_host, x, gamma, at, stats);
+  else
+    hipLaunchKernelGGL(embed_fold_kernel<1>, dim3(B * Tq), dim3(256), 0, st, tokens, tok_emb, pos_emb, Tq, D, state,
+                       pos0_host, x, gamma, at, stats);
+  return hipGetLastError();
+}
+
 // -------------------------------------------------------------- logits --
 // logits[b, v] = sum_d h[b, d] E[v, d]; B <= 32 clips per call.  One wave =
 // 32 vocabulary rows; h staged in LDS in 256-wide k chunks.

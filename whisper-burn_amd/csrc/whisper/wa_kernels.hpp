@@ -64,6 +64,12 @@ hipError_t launch_conv_gelu(const float* in, long in_bs, long in_cs, long in_ts,
 hipError_t launch_embed(const int* tokens, const float* tok_emb, const float* pos_emb, int B, int Tq, int D,
                         const DecodeState* state, int pos0_host, float* x, hipStream_t st);
 
+// launch_embed + the LayerNorm-fold producer for gamma (wq4_gemm_tiled_lnfold):
+// also writes at = A-tiled x * gamma and stats [rows][D/32][2]; D % 32 == 0.
+hipError_t launch_embed_fold(const int* tokens, const float* tok_emb, const float* pos_emb, int B, int Tq, int D,
+                             const DecodeState* state, int pos0_host, float* x, const float* gamma, _Float16* at,
+                             float* stats, int ns, hipStream_t st);
+
 // logits[b, v] = h[b * ldh] . E[v]  (decoder.rs:289-292, 342-343), f32
 // products and accumulation (v_mfma_f32_32x32x2_f32).
 hipError_t launch_logits(const float* h, int B, int D, long ldh, const float* emb, int V, float* logits,

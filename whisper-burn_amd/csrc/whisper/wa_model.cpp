@@ -19,6 +19,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -146,6 +147,11 @@ struct DecLayer {
   float *ln1_w, *ln1_b, *ln2_w, *ln2_b, *ln3_w, *ln3_b;
   float *qkv_b, *out_b, *cq_b, *cv_b, *cout_b, *fc1_b, *fc2_b;
   wq4_tensor *qkv = nullptr, *out = nullptr, *cq = nullptr, *cout = nullptr, *fc1 = nullptr, *fc2 = nullptr;
+  // LayerNorm fold (wq4_gemm_tiled_lnfold) of the GEMMs that read a
+  // LayerNorm: W gamma and W beta + bias of qkv (attn_ln), cq
+  // (cross_attn_ln), fc1 (mlp_ln)
+  float *qkv_wg = nullptr, *qkv_b2 = nullptr, *cq_wg = nullptr, *cq_b2 = nullptr, *fc1_wg = nullptr,
+        *fc1_b2 = nullptr;
   // cross-attention key / value weights in raw GGUF form (Q4_0 blocks or
   // f16), read by the K/V-cache-free cross-attention (wa_xattn.hip)
   uint8_t *ck_raw = nullptr, *cv_raw = nullptr;
@@ -168,6 +174,8 @@ struct DecGroup {
   int *prompt_tok, *next_tok, *tokens, *ntok, *done;
   _Float16* xqt;    // cross-attention Wk^T q operands [rows][ns][16*ceil(H/16)][D]
   float* xattn_part;  // cross-attention split partials (Z, max, sum)
+  _Float16* atd_ln;   // LayerNorm fold: A-tiled x * gamma of the next LayerNorm
+  float* ln_stats;    //                 its per (row, 32-column tile) mean / M2
   float* lg_val;      // fused logits + argmax: per-workgroup candidates [32][groups]
   int *lg_idx, *lg_ctr;
   wa::DecodeState* state;
@@ -518,6 +526,56 @@ wq4_status build_model(wa_model* m, Source& src) {
   return B.st;
 }
 
+// W gamma and W beta + bias of every decoder GEMM that reads a LayerNorm
+// (wq4_ln_fold_vectors, double accumulation from the dequantized weights),
+// layers spread over host threads.
+wq4_status build_ln_fold(wa_model* m) {
+  const int Dt = m->cfg.n_text_state;
+  struct Job {
+    wq4_tensor* w;
+    const float *g, *b, *bias;
+    float **wg, **b2;
+  };
+  std::vector<Job> jobs;
+  for (DecLayer& L : m->dec) {
+    jobs.push_back({L.qkv, L.ln1_w, L.ln1_b, L.qkv_b, &L.qkv_wg, &L.qkv_b2});
+    jobs.push_back({L.cq, L.ln2_w, L.ln2_b, L.cq_b, &L.cq_wg, &L.cq_b2});
+    jobs.push_back({L.fc1, L.ln3_w, L.ln3_b, L.fc1_b, &L.fc1_wg, &L.fc1_b2});
+  }
+  for (Job& j : jobs) {
+    int64_t n = 0, k = 0;
+    (void)wq4_tensor_shape(j.w, &n, &k);
+    *j.wg = m->dev.alloc<float>((size_t)n);
+    *j.b2 = m->dev.alloc<float>((size_t)n);
+    if (!*j.wg || !*j.b2) return fail(WQ4_ENOMEM, "LayerNorm-fold vector allocation failed");
+    m->bytes += (size_t)n * 8;
+  }
+  std::atomic<size_t> next{0};
+  std::atomic<int> bad{0};
+  auto work = [&]() {
+    (void)hipSetDevice(m->device);
+    for (size_t i = next++; i < jobs.size(); i = next++) {
+      const Job& j = jobs[i];
+      int64_t n = 0, k = 0;
+      (void)wq4_tensor_shape(j.w, &n, &k);
+      std::vector<float> g(Dt), b(Dt), bias((size_t)n), wg((size_t)n), b2((size_t)n);
+      if (hipMemcpy(g.data(), j.g, Dt * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+          hipMemcpy(b.data(), j.b, Dt * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+          hipMemcpy(bias.data(), j.bias, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+          wq4_ln_fold_vectors(j.w, g.data(), b.data(), bias.data(), wg.data(), b2.data()) != WQ4_OK ||
+          hipMemcpy(*j.wg, wg.data(), (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(*j.b2, b2.data(), (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess)
+        bad = 1;
+    }
+  };
+  const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) th.emplace_back(work);
+  for (auto& t : th) t.join();
+  if (bad) return fail(WQ4_EHIP, "LayerNorm-fold vectors failed");
+  return WQ4_OK;
+}
+
 wq4_status alloc_activations(wa_model* m) {
   const Config& c = m->cfg;
   const int D = c.n_audio_state, F = 4 * D, Dt = c.n_text_state, Ft = 4 * Dt;
@@ -565,6 +623,8 @@ wq4_status alloc_activations(wa_model* m) {
     g.state = d.alloc<wa::DecodeState>(1);
     g.xattn_part = f32((int64_t)xpart);
     g.xqt = d.alloc<_Float16>((size_t)rdec * m->ns * HP * Dt);
+    g.atd_ln = tiled(rdec, Dt);
+    g.ln_stats = f32(rdec * (Dt / 32) * 2);
     g.lg_val = f32((int64_t)32 * wa::logits_argmax_groups(c.n_vocab));
     g.lg_idx = d.alloc<int>((size_t)32 * wa::logits_argmax_groups(c.n_vocab));
     g.lg_ctr = d.alloc<int>(1);
@@ -572,8 +632,9 @@ wq4_status alloc_activations(wa_model* m) {
     for (void* p : {(void*)g.xd, (void*)g.qkvd, (void*)g.qd, (void*)g.hid, (void*)g.logits, (void*)g.atd_dec,
                     (void*)g.atf_dec, (void*)g.prompt_tok, (void*)g.next_tok, (void*)g.tokens, (void*)g.ntok,
                     (void*)g.done, (void*)g.state, (void*)g.xattn_part, (void*)g.xqt, (void*)g.lg_val,
-                    (void*)g.lg_idx, (void*)g.lg_ctr})
+                    (void*)g.lg_idx, (void*)g.lg_ctr, (void*)g.atd_ln, (void*)g.ln_stats})
       if (!p) return fail(WQ4_ENOMEM, "decode-group allocation failed");
+    WA_HIP(hipMemset(g.atd_ln, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
     WA_HIP(hipMemset(g.lg_ctr, 0, sizeof(int)));
     WA_HIP(hipMemset(g.xqt, 0, (size_t)rdec * m->ns * HP * Dt * 2));  // padded heads stay 0
     WA_HIP(hipMemset(g.atd_dec, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
@@ -689,6 +750,20 @@ wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st) {
   return WQ4_OK;
 }
 
+// LayerNorm fold for this decoder pass: decode steps (Tq = 1) whose GEMMs
+// all run the 8-wave decode plans (WA_LN_FOLD=0 disables, for A/B runs).
+bool lnfold_on(const wa_model* m, int Tq, const wa::DecodeState* state, int64_t rows) {
+  static const bool enabled = [] {
+    const char* e = getenv("WA_LN_FOLD");
+    return e ? atoi(e) != 0 : true;
+  }();
+  if (!enabled || state == nullptr || Tq != 1 || m->dec.empty()) return false;
+  const DecLayer& L = m->dec[0];
+  for (const wq4_tensor* w : {L.qkv, L.out, L.cq, L.cout, L.fc1, L.fc2})
+    if (!wq4_lnfold_supported(w, rows)) return false;
+  return true;
+}
+
 // A greedy decode step of <= 32 clips picks its tokens inside the logits
 // kernel (wa::launch_logits_argmax); prompts and larger groups keep the
 // stored logits + separate argmax.
@@ -707,22 +782,62 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
   const int64_t rows = (int64_t)B * Tq;
   const size_t self_ofs = (size_t)g.b0 * H * c.n_text_ctx * 64;
   const _Float16* enc = m->enc_planes + (size_t)g.b0 * T * m->ns * c.n_audio_state;
-  WA_HIP(wa::launch_embed(tokens, m->tok_emb, m->dec_pos, B, Tq, D, state, pos0, g.xd, st));
-  for (auto& L : m->dec) {  // DecoderBlock (decoder.rs:77-112 / 140-183)
-    WA_WQ4(wq4_layernorm(g.xd, L.ln1_w, L.ln1_b, rows, D, m->prec, g.atd_dec, nullptr, st));
-    WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, g.atd_dec, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, 2, st));
+  // Decode steps fold every decoder LayerNorm into the GEMMs around it
+  // (wq4_gemm_tiled_lnfold): the residual GEMM producing x also writes
+  // tiled(x * gamma) and tile statistics, the GEMM reading LN(x) corrects
+  // its epilogue -- no LayerNorm launches inside the layer loop.
+  const bool fold = lnfold_on(m, Tq, state, rows);
+  if (fold)
+    WA_HIP(wa::launch_embed_fold(tokens, m->tok_emb, m->dec_pos, B, Tq, D, state, pos0, g.xd, m->dec[0].ln1_w,
+                                 g.atd_ln, g.ln_stats, m->ns, st));
+  else
+    WA_HIP(wa::launch_embed(tokens, m->tok_emb, m->dec_pos, B, Tq, D, state, pos0, g.xd, st));
+  const int nl = (int)m->dec.size();
+  for (int li = 0; li < nl; ++li) {  // DecoderBlock (decoder.rs:77-112 / 140-183)
+    DecLayer& L = m->dec[li];
+    if (fold) {
+      const wq4_ln_fold cons1{nullptr, nullptr, nullptr, g.ln_stats, L.qkv_wg};
+      WA_WQ4(wq4_gemm_tiled_lnfold(L.qkv, L.qkv_b2, g.atd_ln, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, &cons1,
+                                   st));
+    } else {
+      WA_WQ4(wq4_layernorm(g.xd, L.ln1_w, L.ln1_b, rows, D, m->prec, g.atd_dec, nullptr, st));
+      WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, g.atd_dec, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, 2, st));
+    }
     WA_HIP(wa::launch_decoder_self_attention(g.qkvd, L.cache_k + self_ofs, L.cache_v + self_ofs, B, Tq, H,
                                              c.n_text_ctx, state, kv0, g.atd_dec, m->ns, st));
-    WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
-    WA_WQ4(wq4_layernorm(g.xd, L.ln2_w, L.ln2_b, rows, D, m->prec, g.atd_dec, nullptr, st));
-    WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, g.atd_dec, nullptr, g.qd, nullptr, rows, 0u, m->prec, 2, st));
+    if (fold) {
+      const wq4_ln_fold prod2{L.ln2_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
+      WA_WQ4(wq4_gemm_tiled_lnfold(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec,
+                                   &prod2, st));
+      const wq4_ln_fold cons2{nullptr, nullptr, nullptr, g.ln_stats, L.cq_wg};
+      WA_WQ4(wq4_gemm_tiled_lnfold(L.cq, L.cq_b2, g.atd_ln, nullptr, g.qd, nullptr, rows, 0u, m->prec, &cons2, st));
+    } else {
+      WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
+      WA_WQ4(wq4_layernorm(g.xd, L.ln2_w, L.ln2_b, rows, D, m->prec, g.atd_dec, nullptr, st));
+      WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, g.atd_dec, nullptr, g.qd, nullptr, rows, 0u, m->prec, 2, st));
+    }
     WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_b, m->wtype, enc, B, Tq, T, H, D, g.xqt, g.xattn_part,
                             g.atd_dec, m->ns, st));
-    WA_WQ4(wq4_gemm_tiled(L.cout, L.cout_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
-    WA_WQ4(wq4_layernorm(g.xd, L.ln3_w, L.ln3_b, rows, D, m->prec, g.atd_dec, nullptr, st));
-    WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, g.atd_dec, nullptr, nullptr, g.atf_dec, rows,
-                          WQ4_EPI_GELU | WQ4_EPI_TILED_OUT, m->prec, 2, st));
-    WA_WQ4(wq4_gemm_tiled(L.fc2, L.fc2_b, g.atf_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
+    if (fold) {
+      const wq4_ln_fold prod3{L.ln3_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
+      WA_WQ4(wq4_gemm_tiled_lnfold(L.cout, L.cout_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL,
+                                   m->prec, &prod3, st));
+      const wq4_ln_fold cons3{nullptr, nullptr, nullptr, g.ln_stats, L.fc1_wg};
+      WA_WQ4(wq4_gemm_tiled_lnfold(L.fc1, L.fc1_b2, g.atd_ln, nullptr, nullptr, g.atf_dec, rows,
+                                   WQ4_EPI_GELU | WQ4_EPI_TILED_OUT, m->prec, &cons3, st));
+      // the next layer's attn_ln (none after the last layer: decoder.ln below)
+      const wq4_ln_fold prod1{li + 1 < nl ? m->dec[li + 1].ln1_w : nullptr, li + 1 < nl ? g.atd_ln : nullptr,
+                              li + 1 < nl ? g.ln_stats : nullptr, nullptr, nullptr};
+      WA_WQ4(wq4_gemm_tiled_lnfold(L.fc2, L.fc2_b, g.atf_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec,
+                                   &prod1, st));
+    } else {
+      WA_WQ4(wq4_gemm_tiled(L.cout, L.cout_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2,
+                            st));
+      WA_WQ4(wq4_layernorm(g.xd, L.ln3_w, L.ln3_b, rows, D, m->prec, g.atd_dec, nullptr, st));
+      WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, g.atd_dec, nullptr, nullptr, g.atf_dec, rows,
+                            WQ4_EPI_GELU | WQ4_EPI_TILED_OUT, m->prec, 2, st));
+      WA_WQ4(wq4_gemm_tiled(L.fc2, L.fc2_b, g.atf_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
+    }
   }
   // final LN (decoder.rs:286 / 340) and tied-embedding logits of the last
   // position of every clip (decoder.rs:289-292, 342-343)
@@ -867,6 +982,8 @@ wq4_status wa_model_create_synthetic_ex(int device, int variant, uint64_t seed, 
   SynthSource src(seed);
   wq4_status s = build_model(m.get(), src);
   if (s != WQ4_OK) return s;
+  s = build_ln_fold(m.get());
+  if (s != WQ4_OK) return s;
   s = alloc_activations(m.get());
   if (s != WQ4_OK) return s;
   WA_HIP(hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking));
@@ -900,6 +1017,8 @@ wq4_status wa_model_create_from_gguf(int device, const char* path, int variant, 
   m->wtype = probe && probe->type == wa::kGgmlF16 ? 1 : 0;  // an F16 checkpoint (config 5)
   GgufSource src(file);
   wq4_status s = build_model(m.get(), src);
+  if (s != WQ4_OK) return s;
+  s = build_ln_fold(m.get());
   if (s != WQ4_OK) return s;
   s = alloc_activations(m.get());
   if (s != WQ4_OK) return s;

@@ -632,6 +632,73 @@ wq4_status wq4_gemm_ln_tiled(const wq4_tensor* w, const float* bias_dev, const f
                         flags & ~WQ4_EPI_LN_FUSED, prec, kernel, stream);
 }
 
+int wq4_lnfold_supported(const wq4_tensor* w, int64_t rows) {
+  if (!w || w->flat || rows < 1 || rows > 32 * wq4::kDecodeMaxMTiles) return 0;
+  return wq4::decode_ln_supported(w->g, (int)rows) ? 1 : 0;
+}
+
+wq4_status wq4_gemm_tiled_lnfold(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
+                                 const float* residual_dev, float* y_dev, void* at_out_dev, int64_t rows,
+                                 unsigned flags, wq4_precision prec, const wq4_ln_fold* fold, void* stream) {
+  wq4_status s = check_gemm_tensor(w);
+  if (s != WQ4_OK) return s;
+  s = check_prec(prec);
+  if (s != WQ4_OK) return s;
+  if (!fold) return fail(WQ4_EINVAL, "fold is null");
+  if (rows == 0) return WQ4_OK;
+  if (!wq4_lnfold_supported(w, rows)) return fail(WQ4_ESHAPE, "LayerNorm fold needs a decode-sized 8-wave plan");
+  const bool tiled_out = (flags & WQ4_EPI_TILED_OUT) != 0;
+  const bool producer = fold->at_out_dev != nullptr, consumer = fold->stats_in_dev != nullptr;
+  if (!at_dev || (tiled_out ? !at_out_dev : !y_dev)) return fail(WQ4_EINVAL, "null argument");
+  if ((flags & WQ4_EPI_RESIDUAL) && (!residual_dev || tiled_out))
+    return fail(WQ4_EINVAL, "WQ4_EPI_RESIDUAL needs a residual and an f32 output");
+  if (producer && (!fold->gamma_dev || !fold->stats_out_dev || tiled_out || w->g.n % 32 != 0 || w->g.n > 2048))
+    return fail(WQ4_EINVAL, "LayerNorm-fold producer needs gamma, statistics, an f32 output and N % 32 == 0");
+  if (consumer && (!fold->wg_dev || w->g.k % 32 != 0 || w->g.k / 32 > 64))
+    return fail(WQ4_EINVAL, "LayerNorm-fold consumer needs W gamma and K % 32 == 0, K <= 2048");
+  if (tiled_out && w->g.n % 32 != 0) return fail(WQ4_ESHAPE, "tiled output needs N % 32 == 0");
+  DeviceGuard dg(w->device);
+  wq4::EpiArgs epi = make_epi(bias_dev, (flags & WQ4_EPI_RESIDUAL) ? residual_dev : nullptr, y_dev, (int)w->g.n,
+                              (int)rows, (int)w->g.n, (flags & WQ4_EPI_GELU) != 0);
+  if (tiled_out) {
+    epi.out_tiled = static_cast<_Float16*>(at_out_dev);
+    epi.nbp_next = (int)((w->g.n / 32 + 1) / 2);
+  }
+  if (producer) {
+    epi.lnf_g = fold->gamma_dev;
+    epi.lnf_at = static_cast<_Float16*>(fold->at_out_dev);
+    epi.lnf_stats_out = fold->stats_out_dev;
+    epi.lnf_nbp = (int)((w->g.n / 32 + 1) / 2);
+  }
+  if (consumer) {
+    epi.lnf_stats_in = fold->stats_in_dev;
+    epi.lnf_wg = fold->wg_dev;
+    epi.lnf_tiles = (int)(w->g.k / 32);
+  }
+  return gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, tiled_out ? wq4::kEpiTiled : wq4::kEpiF32,
+              ns_of(prec), static_cast<hipStream_t>(stream), true);
+}
+
+wq4_status wq4_ln_fold_vectors(const wq4_tensor* w, const float* gamma, const float* beta, const float* bias,
+                               float* wg_out, float* bias_out) {
+  if (!w || !gamma || !beta || !wg_out || !bias_out) return fail(WQ4_EINVAL, "null argument");
+  const int64_t n = w->g.n, k = w->g.k;
+  std::vector<float> wd((size_t)(n * k));
+  wq4_status s = wq4_tensor_dequantize(w, wd.data());
+  if (s != WQ4_OK) return s;
+  for (int64_t i = 0; i < n; ++i) {
+    const float* row = wd.data() + i * k;
+    double sg = 0.0, sb = 0.0;
+    for (int64_t j = 0; j < k; ++j) {
+      sg += (double)row[j] * gamma[j];
+      sb += (double)row[j] * beta[j];
+    }
+    wg_out[i] = (float)sg;
+    bias_out[i] = (float)(sb + (bias ? (double)bias[i] : 0.0));
+  }
+  return WQ4_OK;
+}
+
 wq4_status wq4_prepare_stream(int device, void* stream) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return fail(WQ4_EINVAL, "bad device");

@@ -24,6 +24,22 @@ struct EpiArgs {
   const float* lng;
   const float* lnb;
   int lnd;
+  // LayerNorm folded into the GEMMs around it (decode kernel, 8-wave plans;
+  // wq4_gemm_tiled_lnfold).  Producer (a residual GEMM whose output x feeds
+  // LayerNorm(x; gamma, beta)): also writes the A-tiled operand of x * gamma
+  // (lnf_at, K' = N, lnf_nbp block pairs) and per (row, 32-column tile) the
+  // tile mean and sum of squared deviations (lnf_stats_out [M][N/32][2]).
+  // Consumer (a GEMM on LayerNorm(x)): A = tiled(x * gamma); merges the
+  // lnf_tiles tile statistics of each row (Chan et al.) and applies
+  // out = (acc - mean * lnf_wg[n]) / sqrt(var + 1e-5) + bias[n] before the
+  // rest of the epilogue (bias = W beta + linear bias, lnf_wg = W gamma).
+  const float* lnf_g;
+  _Float16* lnf_at;
+  float* lnf_stats_out;
+  int lnf_nbp;
+  const float* lnf_stats_in;
+  const float* lnf_wg;
+  int lnf_tiles;
 };
 
 // Output element index.  Row-major by default; head-major (hm_t > 0) writes

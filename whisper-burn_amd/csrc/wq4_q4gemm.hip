@@ -421,13 +421,34 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
   // are not a memory round trip after the MFMAs (bias, residual: never
   // written by this launch before its own epilogue reads them).
   float pre_bias = 0.0f, pre_res[2] = {0.0f, 0.0f};
+  float pre_wg = 0.0f, pre_g = 0.0f;  // LayerNorm fold: W gamma[col] (consumer), gamma[col] (producer)
   if constexpr (W == 8 && EPI != kEpiHeadMajor) {
     const int col = nt * 32 + r;
     if (e.bias && col < e.n) pre_bias = e.bias[col];
+    if (e.lnf_stats_in && col < e.n) pre_wg = e.lnf_wg[col];
+    if (e.lnf_at && col < e.n) pre_g = e.lnf_g[col];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int row = mt0 * 32 + acc_row(2 * wave + q, lane >> 5);
       if (e.residual && row < e.m && col < e.n) pre_res[q] = e.residual[(size_t)row * e.ldo + col];
+    }
+  }
+  // LayerNorm fold, consumer: thread (row tid / 16, part tid % 16) loads the
+  // row's tile statistics j = part, part + 16, ... first, so they land before
+  // the weight / operand stream; merged below while that stream is in flight.
+  constexpr int kLnfPer = 4;  // <= 64 tiles (D <= 2048)
+  floatx2 lnf_st[kLnfPer];
+  const int lnf_row = tid >> 4, lnf_part = tid & 15;
+  if constexpr (W == 8) {
+    if (e.lnf_stats_in) {
+      const int grow = mt0 * 32 + lnf_row;
+#pragma unroll
+      for (int u = 0; u < kLnfPer; ++u) {
+        const int j = lnf_part + 16 * u;
+        lnf_st[u] = (grow < e.m && j < e.lnf_tiles)
+                        ? *reinterpret_cast<const floatx2*>(e.lnf_stats_in + ((size_t)grow * e.lnf_tiles + j) * 2)
+                        : floatx2{0.0f, 0.0f};
+      }
     }
   }
 
@@ -546,6 +567,46 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
     }
   }
 
+  // LayerNorm fold, consumer: Chan et al. merge of the row's tile
+  // statistics (every tile 32 columns), then over the 16 parts of the row by
+  // a butterfly in which the lower lane is always the left operand, so every
+  // lane -- and every workgroup of the launch -- gets the same bits.
+  float* lnf_mu = reinterpret_cast<float*>(smem + decode_lds_bytes_dev(W) + 2 * 64 * 4);  // [32]
+  float* lnf_den = lnf_mu + 32;                                                           // [32]
+  float* lnf_x = lnf_den + 32;                                                            // [32][33]
+  if constexpr (W == 8) {
+    if (e.lnf_stats_in) {
+      float n_a = 0.0f, m_a = 0.0f, q_a = 0.0f;
+#pragma unroll
+      for (int u = 0; u < kLnfPer; ++u) {
+        if (lnf_part + 16 * u < e.lnf_tiles) {
+          const float n = n_a + 32.0f, d = lnf_st[u][0] - m_a;
+          m_a = m_a + d * (32.0f / n);
+          q_a = q_a + lnf_st[u][1] + d * d * (n_a * 32.0f / n);
+          n_a = n;
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float n_b = __shfl_xor(n_a, o, 64), m_b = __shfl_xor(m_a, o, 64), q_b = __shfl_xor(q_a, o, 64);
+        const bool low = (lnf_part & o) == 0;
+        const float nl = low ? n_a : n_b, ml = low ? m_a : m_b, ql = low ? q_a : q_b;
+        const float nh = low ? n_b : n_a, mh = low ? m_b : m_a, qh = low ? q_b : q_a;
+        const float n = nl + nh;
+        if (n > 0.0f) {
+          const float d = mh - ml;
+          m_a = ml + d * (nh / n);
+          q_a = ql + qh + d * d * (nl * nh / n);
+        }
+        n_a = n;
+      }
+      if (lnf_part == 0) {
+        lnf_mu[lnf_row] = m_a;
+        lnf_den[lnf_row] = sqrtf(q_a / (float)(32 * e.lnf_tiles) + 1e-5f);
+      }
+    }
+  }
+
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     floatx16 acc0, acc1;
@@ -638,19 +699,52 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
         const int i = 2 * wave + q;
         const int rl = acc_row(i, h);
         const int row = (mt0 + mt) * 32 + rl;
+        float a = v[q] * cs;
+        if (e.lnf_stats_in) a = (a - lnf_mu[rl] * pre_wg) / lnf_den[rl];  // LayerNorm fold, consumer
         if constexpr (EPI == kEpiTiled) {
-          stage[rl * kStageLd + r] =
-              (row < e.m && col < e.n) ? epi_value_pre(v[q] * cs, pre_bias, pre_res[q], e) : 0.0f;
+          stage[rl * kStageLd + r] = (row < e.m && col < e.n) ? epi_value_pre(a, pre_bias, pre_res[q], e) : 0.0f;
         } else if constexpr (EPI == kEpiHeadMajor) {
-          if (row < e.m && col < e.n) e.out[out_index(e, row, col)] = epi_value(v[q] * cs, row, col, e);
+          if (row < e.m && col < e.n) e.out[out_index(e, row, col)] = epi_value(a, row, col, e);
         } else {
-          if (row < e.m && col < e.n)
-            e.out[(size_t)row * e.ldo + col] = epi_value_pre(v[q] * cs, pre_bias, pre_res[q], e);
+          const bool ok = row < e.m && col < e.n;
+          const float y = epi_value_pre(a, pre_bias, pre_res[q], e);
+          if (ok) e.out[(size_t)row * e.ldo + col] = y;
+          if (e.lnf_at) {  // LayerNorm fold, producer: x (statistics) and x * gamma (next operand)
+            lnf_x[rl * 33 + r] = ok ? y : 0.0f;
+            stage[rl * kStageLd + r] = ok ? y * pre_g : 0.0f;
+          }
         }
       }
       if constexpr (EPI == kEpiTiled) {
         __syncthreads();
         if (wave == 0) store_tiled_slab<NS, 1>(stage, e, mt0 + mt, nt, lane);
+      }
+      if constexpr (EPI == kEpiF32) {
+        if (e.lnf_at) {
+          __syncthreads();
+          if (wave == 0) {
+            EpiArgs e2 = e;
+            e2.out_tiled = e.lnf_at;
+            e2.nbp_next = e.lnf_nbp;
+            store_tiled_slab<NS, 1>(stage, e2, mt0 + mt, nt, lane);
+          } else if (wave == 1 && lane < 32) {
+            const int row = (mt0 + mt) * 32 + lane;
+            if (row < e.m) {
+              float sum = 0.0f;
+#pragma unroll
+              for (int c = 0; c < 32; ++c) sum += lnf_x[lane * 33 + c];
+              const float mean = sum * (1.0f / 32.0f);
+              float m2 = 0.0f;
+#pragma unroll
+              for (int c = 0; c < 32; ++c) {
+                const float d = lnf_x[lane * 33 + c] - mean;
+                m2 += d * d;
+              }
+              *reinterpret_cast<floatx2*>(e.lnf_stats_out + ((size_t)row * (e.n / 32) + nt) * 2) =
+                  floatx2{mean, m2};
+            }
+          }
+        }
       }
       if (ks > 1 && tid == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
       continue;  // MT == 1 for 8-wave plans
@@ -738,7 +832,8 @@ static size_t prefill_lds_bytes(int ns, int epi) {
   return a > s ? a : s;
 }
 
-static size_t decode_lds_bytes(int w) { return decode_lds_bytes_dev(w) + 2 * 64 * 4; }  // + LNA row stats
+// + LNA row stats, + LayerNorm-fold mean / den [32] each and the producer's x stage [32][33]
+static size_t decode_lds_bytes(int w) { return decode_lds_bytes_dev(w) + 2 * 64 * 4 + (64 + 32 * 33) * 4; }
 
 DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal) {
   // Smallest per-wave depth whose grid still covers ~all CUs, then balance.

@@ -90,7 +90,10 @@ def _declare(L: ctypes.CDLL) -> None:
     L.wq4_layernorm.argtypes = [vp, vp, vp, c_i64, c_i64, c_int, vp, vp, vp]
     L.wq4_prepare_stream.argtypes = [c_int, vp]
     L.wq4_gemm_ln_tiled.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, c_i64, ctypes.c_uint, c_int, c_int, vp]
-    for name in ("wq4_gemm_ln_tiled", "wq4_tile_activations", "wq4_linear_forward_tiled", "wq4_linear_forward_tiled_out", "wq4_gemm_tiled",
+    L.wq4_gemm_tiled_lnfold.argtypes = [vp, vp, vp, vp, vp, vp, c_i64, ctypes.c_uint, c_int, ctypes.POINTER(LnFold), vp]
+    L.wq4_ln_fold_vectors.argtypes = [vp, f32p, f32p, f32p, f32p, f32p]
+    L.wq4_lnfold_supported.argtypes = [vp, c_i64]
+    for name in ("wq4_gemm_tiled_lnfold", "wq4_ln_fold_vectors", "wq4_lnfold_supported", "wq4_gemm_ln_tiled", "wq4_tile_activations", "wq4_linear_forward_tiled", "wq4_linear_forward_tiled_out", "wq4_gemm_tiled",
                  "wq4_gemm_tiled_headmajor", "wq4_layernorm", "wq4_prepare_stream"):
         getattr(L, name).restype = c_int
     for name in ("wq4_device_count", "wq4_set_precision", "wq4_set_kernel_policy", "wq4_tensor_create",
@@ -98,6 +101,12 @@ def _declare(L: ctypes.CDLL) -> None:
                  "wq4_linear_forward", "wq4_ffn_forward", "wq4_linear_forward_ws", "wq4_ffn_forward_ws",
                  "wq4_debug_repack", "wq4_debug_unrepack", "wq4_debug_repacked_bytes", "wq4_quantize_q4_0", "wq4_tensor_create_f16"):
         getattr(L, name).restype = c_int
+
+
+class LnFold(ctypes.Structure):
+    """wq4_ln_fold (include/wq4.h): LayerNorm folded into the GEMMs around it."""
+    _fields_ = [("gamma_dev", ctypes.c_void_p), ("at_out_dev", ctypes.c_void_p), ("stats_out_dev", ctypes.c_void_p),
+                ("stats_in_dev", ctypes.c_void_p), ("wg_dev", ctypes.c_void_p)]
 
 
 def lib() -> ctypes.CDLL:
