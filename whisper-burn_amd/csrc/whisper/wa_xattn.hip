@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void xattn_q_kernel(const float* __restrict__ 
 // heads, k = the 16 frames read transposed from the same LDS image by
 // ds_read_b64_tr_b16; accumulators stay in registers).  Writes per (row,
 // split): Z [H][D] and (max, sum) [H].
-template <int D, int HT, int NS, int NW, int PF>
+template <int D, int HT, int NS, int NW, int PF, int AUX = 0, int MODE = 0>
 __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __restrict__ qt,
                                                              const _Float16* __restrict__ enc, int Tq, int T,
                                                              int H, int S, int CH, float* __restrict__ zpart,
@@ -175,6 +175,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   __shared__ float red[NW][HT][16][17];
   __shared__ __attribute__((aligned(16))) _Float16 sp[NS][32][kTc];
   __shared__ float salpha[32];
+  __shared__ int srescale[2];
   __shared__ __attribute__((aligned(16))) _Float16 sq1[HT == 2 ? NS : 1][4][HT == 2 ? D + 16 : 8];
 
   const int s = blockIdx.x, r = blockIdx.y;
@@ -208,6 +209,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   // rows of P past the score tiles stay 0, their alpha 1
   for (int i = tid; i < NS * 32 * kTc; i += kThreads) (&sp[0][0][0])[i] = (_Float16)0.0f;
   if (tid < 32) salpha[tid] = 1.0f;
+  if (tid < 2) srescale[tid] = 0;
 
   floatx16 zacc[KS];
 #pragma unroll
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
       const int v = tid + i * kThreads;
       const int row = v / (ROW / 8), col = v - row * (ROW / 8);
       const uint32_t off = v < NV ? (uint32_t)((chi * kTc + row) * ROW * 2 + col * 16) : 0x7fffff00u;
-      buf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+      buf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUX);
     }
   };
 
@@ -245,6 +247,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   const int g = l >> 4, gi = l & 15;
   const int trow = 8 * (g >> 1) + (gi >> 2), tcol = 16 * (g & 1) + 4 * (gi & 3);
 
+  float sink = 0.0f;
   auto step = [&](u32x4v (&buf)[NLD], int chi) {
     const int t0 = ts + chi * kTc;
     __syncthreads();  // previous sub-chunk's readers are done with se / sp
@@ -255,7 +258,11 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
       if (v < NV) *reinterpret_cast<u32x4v*>(&se[row * RS + col * 8]) = buf[i];
     }
     __syncthreads();
-    if (chi + PF < nch) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
+    if (MODE != 2 && chi + PF < nch) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
+    if constexpr (MODE == 1) {  // probe: the load / LDS-write skeleton alone (one LDS read keeps it live)
+      sink += (float)se[(tid * 9) % (kTc * RS)];
+      return;
+    }
 
     // scores of this wave's column slice: A = enc (m = frame, k = column),
     // B = qt (k = column, n = head)
@@ -324,19 +331,26 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
         sp[0][h][t] = phi;
         if (NS == 2) sp[1][h][t] = plo;
         if (t == 0) salpha[h] = alpha;
+        if (alpha != 1.0f) srescale[chi & 1] = 1;  // benign race: every writer stores 1
       }
     }
     __syncthreads();
+    // alpha == 1 for every head (no running maximum moved, the steady state)
+    // makes the rescale a multiplication by 1: skipped, bit-identical
+    const bool rescale = srescale[chi & 1] != 0;
+    if (tid == 0) srescale[(chi + 1) & 1] = 0;  // next sub-chunk's flag; its writers come after two barriers
 
     // Z update: A = P (m = head, k = frame), B = enc (k = frame, n = column)
     half8 pa[NS];
 #pragma unroll
     for (int p = 0; p < NS; ++p) pa[p] = *reinterpret_cast<const half8*>(&sp[p][l32][8 * lh]);
+    if (rescale) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float al = salpha[(j & 3) + 8 * (j >> 2) + 4 * lh];
+      for (int j = 0; j < 16; ++j) {
+        const float al = salpha[(j & 3) + 8 * (j >> 2) + 4 * lh];
 #pragma unroll
-      for (int ct = 0; ct < KS; ++ct) zacc[ct][j] *= al;
+        for (int ct = 0; ct < KS; ++ct) zacc[ct][j] *= al;
+      }
     }
 #pragma unroll
     for (int ct = 0; ct < KS; ++ct) {
@@ -369,6 +383,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     for (int chi = 0; chi < nch; ++chi) step(pre0, chi);
   }
 
+  if constexpr (MODE == 1) zacc[0][0] += sink * 1e-30f;
   // partials of this (row, split)
   const size_t base = (size_t)r * S + s;
 #pragma unroll
@@ -564,13 +579,19 @@ __global__ __launch_bounds__(256) void untile_kernel(const _Float16* __restrict_
 template <int D, int HT, int NS>
 void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T, int H, int S, int CH, float* z,
                  float* ml, hipStream_t st) {
-  static const int variant = [] {  // tuning knob: 0 = 8 waves / 1 sub-chunk in flight, 1 = 4 waves / 2
+  static const int variant = [] {  // probe knob: 1 = the load skeleton alone (wrong results)
     const char* e = getenv("WA_XATTN_MAIN");
     return e ? atoi(e) : 0;
   }();
   if constexpr ((D / 8) % 32 == 0) {
-    if (variant == 1) {
-      hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 4, 2>), g, dim3(256), 0, st, qt, enc, Tq, T, H, S, CH, z, ml);
+    if (variant == 2) {  // probe (wrong results): compute on the first sub-chunk only, no further loads
+      hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1, 0, 2>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z,
+                         ml);
+      return;
+    }
+    if (variant == 1) {  // probe (wrong results): loads + LDS writes + barriers only
+      hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1, 0, 1>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z,
+                         ml);
       return;
     }
     hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z, ml);
