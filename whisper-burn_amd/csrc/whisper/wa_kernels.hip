@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <cstdlib>
 
 #include "../wq4_device.hpp"
 #include "../wq4_lnmath.hpp"
@@ -42,6 +43,7 @@ __device__ __forceinline__ floatx16 mfma_f32(float a, float b, const floatx16& c
 
 using wq4::atile_store4;
 using wq4::kbp_of;
+using wq4::split_f16;
 
 
 
@@ -146,13 +148,224 @@ __global__ __launch_bounds__(256) void encoder_attention_kernel(const float* __r
   }
 }
 
+// ------------------------------------ encoder attention, f16x2 MFMA --
+// Same contract as encoder_attention_kernel (attention.rs:243-298,
+// non-causal), products on v_mfma_f32_32x32x16_f16 with every operand an
+// exact-to-2^-22 f16 pair (x = hi + lo; hi*hi + lo*hi + hi*lo, f32
+// accumulation -- the arithmetic of the Q4 GEMMs), 3 MFMAs per product
+// instead of the f32 MFMA's 16x slower rate.  Workgroup = 4 waves x 32
+// queries of one (clip, head); 64-key tiles of K and V are converted to f16
+// pairs into LDS (row stride 72 halves: conflict-free b128 and transposed
+// reads), the next tile's f32 loads in flight meanwhile.
+//   S^T = K Q^T   A = K (m = key, k = dim) ds_read_b128; B = Q^T from registers
+//   O^T += V^T P^T  A = V^T via ds_read_b64_tr_b16 of row-major V, in the key
+//                 order of the S^T accumulator; B = P^T = that accumulator.
+typedef _Float16 ea_half4 __attribute__((ext_vector_type(4)));
+typedef __fp16 ea_fp16x4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
+__device__ __forceinline__ ea_half4 ea_tr4(const _Float16* p) {
+  return __builtin_bit_cast(ea_half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+                                          (__attribute__((address_space(3))) ea_fp16x4*)(p)));
+}
+__device__ __forceinline__ floatx16 ea_mfma(half8 a, half8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+constexpr int kEaKeys = 64;  // keys per LDS tile
+constexpr int kEaLd = 72;    // LDS row stride (halves)
+
+template <int NS>
+__global__ __launch_bounds__(256) void encoder_attention_f16_kernel(const float* __restrict__ qkv, int T, int H,
+                                                                    _Float16* __restrict__ tiled) {
+  __shared__ __attribute__((aligned(16))) _Float16 kls[NS][kEaKeys * kEaLd];
+  __shared__ __attribute__((aligned(16))) _Float16 vls[NS][kEaKeys * kEaLd];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, lh = lane >> 5;
+  const int head = blockIdx.y, b = blockIdx.z;
+  const int D = H * 64, ld = 3 * D;
+  const float* base = qkv + (size_t)b * T * ld;
+  const int q = blockIdx.x * 128 + wave * 32 + l32;
+
+  // Q^T operand (k = dim, n = query): lane (query l32, dims 16 ks + 8 lh + 0..7), scaled by 1/8 (exact)
+  half8 qb[4][NS];
+  {
+    const float* qr = base + (size_t)(q < T ? q : 0) * ld + head * 64;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const floatx4 x0 = *reinterpret_cast<const floatx4*>(qr + 16 * ks + 8 * lh);
+      const floatx4 x1 = *reinterpret_cast<const floatx4*>(qr + 16 * ks + 8 * lh + 4);
+      half8 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = q < T ? (j < 4 ? x0[j] : x1[j - 4]) * 0.125f : 0.0f;
+        _Float16 a, c;
+        split_f16(v, a, c);
+        hi[j] = a;
+        lo[j] = c;
+      }
+      qb[ks][0] = hi;
+      if constexpr (NS == 2) qb[ks][1] = lo;
+    }
+  }
+  // staging: thread (key tid / 4, dims 16 (tid % 4) + 0..15) of K and V
+  const int skey = tid >> 2, sd = (tid & 3) * 16;
+  floatx4 kreg[4], vreg[4];
+  auto fetch = [&](int key0) {
+    const int key = key0 + skey;
+    const bool ok = key < T;
+    const float* kr = base + (size_t)(ok ? key : 0) * ld + D + head * 64 + sd;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      kreg[i] = ok ? *reinterpret_cast<const floatx4*>(kr + 4 * i) : floatx4{0.f, 0.f, 0.f, 0.f};
+      vreg[i] = ok ? *reinterpret_cast<const floatx4*>(kr + D + 4 * i) : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto stage = [&]() {
+    half8 kh[2], kl[2], vh[2], vl[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      _Float16 a, c;
+      split_f16(kreg[i >> 2][i & 3], a, c);
+      kh[i >> 3][i & 7] = a;
+      kl[i >> 3][i & 7] = c;
+      split_f16(vreg[i >> 2][i & 3], a, c);
+      vh[i >> 3][i & 7] = a;
+      vl[i >> 3][i & 7] = c;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      *reinterpret_cast<half8*>(&kls[0][skey * kEaLd + sd + 8 * u]) = kh[u];
+      *reinterpret_cast<half8*>(&vls[0][skey * kEaLd + sd + 8 * u]) = vh[u];
+      if constexpr (NS == 2) {
+        *reinterpret_cast<half8*>(&kls[NS - 1][skey * kEaLd + sd + 8 * u]) = kl[u];
+        *reinterpret_cast<half8*>(&vls[NS - 1][skey * kEaLd + sd + 8 * u]) = vl[u];
+      }
+    }
+  };
+
+  float m = -INFINITY, l = 0.0f;
+  floatx16 o[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    o[0][i] = 0.0f;
+    o[1][i] = 0.0f;
+  }
+  // transposed-read geometry: 16-lane group g = lane / 16 covers dims
+  // 16 (g & 1) + 0..15 and keys 4 (g >> 1) + 0..3 (+ 8): the S^T
+  // accumulator's key order for lanes < 32 / >= 32
+  const int g = lane >> 4, gi = lane & 15;
+  const int trow = 4 * (g >> 1) + (gi >> 2), tcol = 16 * (g & 1) + 4 * (gi & 3);
+  const int ntile = (T + kEaKeys - 1) / kEaKeys;
+  fetch(0);
+  for (int kt = 0; kt < ntile; ++kt) {
+    const int key0 = kt * kEaKeys;
+    __syncthreads();  // previous tile's readers are done
+    stage();
+    __syncthreads();
+    if (kt + 1 < ntile) fetch(key0 + kEaKeys);  // next tile in flight during this one
+#pragma unroll
+    for (int sub = 0; sub < kEaKeys / 32; ++sub) {
+      floatx16 st;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st[i] = 0.0f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int off = (sub * 32 + l32) * kEaLd + 16 * ks + 8 * lh;
+        const half8 ah = *reinterpret_cast<const half8*>(&kls[0][off]);
+        st = ea_mfma(ah, qb[ks][0], st);
+        if constexpr (NS == 2) {
+          const half8 al = *reinterpret_cast<const half8*>(&kls[1][off]);
+          st = ea_mfma(al, qb[ks][0], st);
+          st = ea_mfma(ah, qb[ks][1], st);
+        }
+      }
+      // online softmax of query l32 over these 32 keys (16 here, 16 in lane ^ 32)
+      float mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = key0 + sub * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+        if (key >= T) st[i] = -INFINITY;
+        mx = fmaxf(mx, st[i]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float alpha = expf(m - mn);
+      float rs = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        st[i] = expf(st[i] - mn);
+        rs += st[i];
+      }
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = mn;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        o[0][i] *= alpha;
+        o[1][i] *= alpha;
+      }
+      // P^T operands: MFMA t takes accumulator registers 8 t .. 8 t + 7
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        half8 ph, pl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          _Float16 a, c;
+          split_f16(st[8 * t + j], a, c);
+          ph[j] = a;
+          pl[j] = c;
+        }
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          half8 va[NS];
+#pragma unroll
+          for (int pp = 0; pp < NS; ++pp) {
+            const _Float16* vb = &vls[pp][(sub * 32 + 16 * t + trow) * kEaLd + dt * 32 + tcol];
+            const ea_half4 x0 = ea_tr4(vb);
+            const ea_half4 x1 = ea_tr4(vb + 8 * kEaLd);
+            va[pp] = half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+          }
+          o[dt] = ea_mfma(va[0], ph, o[dt]);
+          if constexpr (NS == 2) {
+            o[dt] = ea_mfma(va[1], ph, o[dt]);
+            o[dt] = ea_mfma(va[0], pl, o[dt]);
+          }
+        }
+      }
+    }
+  }
+  if (q < T) {
+    const int row = b * T + q;
+    const int kbp = kbp_of(D);
+    const float inv = 1.0f / l;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d = dt * 32 + 8 * gg + 4 * lh;
+        atile_store4<NS>(tiled, row, head * 64 + d, kbp, o[dt][4 * gg] * inv, o[dt][4 * gg + 1] * inv,
+                         o[dt][4 * gg + 2] * inv, o[dt][4 * gg + 3] * inv);
+      }
+  }
+}
+
 hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Float16* tiled, int ns,
                                     hipStream_t st) {
   const dim3 grid((T + 127) / 128, H, B), block(256);
-  if (ns == 2)
-    hipLaunchKernelGGL((encoder_attention_kernel<2>), grid, block, 0, st, qkv, T, H, tiled);
-  else
-    hipLaunchKernelGGL((encoder_attention_kernel<1>), grid, block, 0, st, qkv, T, H, tiled);
+  static const bool f32_mfma = [] {  // WA_ENC_ATTN_F32=1: the f32-MFMA kernel (A/B, diagnostics)
+    const char* e = getenv("WA_ENC_ATTN_F32");
+    return e && atoi(e) != 0;
+  }();
+  if (f32_mfma) {
+    if (ns == 2)
+      hipLaunchKernelGGL((encoder_attention_kernel<2>), grid, block, 0, st, qkv, T, H, tiled);
+    else
+      hipLaunchKernelGGL((encoder_attention_kernel<1>), grid, block, 0, st, qkv, T, H, tiled);
+  } else {
+    if (ns == 2)
+      hipLaunchKernelGGL((encoder_attention_f16_kernel<2>), grid, block, 0, st, qkv, T, H, tiled);
+    else
+      hipLaunchKernelGGL((encoder_attention_f16_kernel<1>), grid, block, 0, st, qkv, T, H, tiled);
+  }
   return hipGetLastError();
 }
 
