@@ -248,24 +248,9 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   const int trow = 8 * (g >> 1) + (gi >> 2), tcol = 16 * (g & 1) + 4 * (gi & 3);
 
   float sink = 0.0f;
-  auto step = [&](u32x4v (&buf)[NLD], int chi) {
-    const int t0 = ts + chi * kTc;
-    __syncthreads();  // previous sub-chunk's readers are done with se / sp
-#pragma unroll
-    for (int i = 0; i < NLD; ++i) {
-      const int v = tid + i * kThreads;
-      const int row = v / (ROW / 8), col = v - row * (ROW / 8);
-      if (v < NV) *reinterpret_cast<u32x4v*>(&se[row * RS + col * 8]) = buf[i];
-    }
-    __syncthreads();
-    if (MODE != 2 && chi + PF < nch) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
-    if constexpr (MODE == 1) {  // probe: the load / LDS-write skeleton alone (one LDS read keeps it live)
-      sink += (float)se[(tid * 9) % (kTc * RS)];
-      return;
-    }
-
-    // scores of this wave's column slice: A = enc (m = frame, k = column),
-    // B = qt (k = column, n = head)
+  // scores of this wave's column slice: A = enc (m = frame, k = column) from
+  // afrag(ks, plane), B = qt (k = column, n = head); partial sums to red
+  auto scores = [&](auto&& afrag) {
     floatx4 sacc[HT];
 #pragma unroll
     for (int ht = 0; ht < HT; ++ht) sacc[ht] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -273,8 +258,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     for (int ks = 0; ks < KS; ++ks) {
       half8 a[NS];
 #pragma unroll
-      for (int p = 0; p < NS; ++p)
-        a[p] = *reinterpret_cast<const half8*>(&se[l16 * RS + p * D + c0 + ks * 32 + 8 * lq]);
+      for (int p = 0; p < NS; ++p) a[p] = afrag(ks, p);
 #pragma unroll
       for (int ht = 0; ht < HT; ++ht) {
         half8 b[NS];
@@ -300,6 +284,9 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
       for (int j = 0; j < 4; ++j) red[w][ht][l16][4 * lq + j] = sacc[ht][j];
     __syncthreads();
 
+  };
+  // online softmax of the sub-chunk's scores (red) and the Z update from se
+  auto tail = [&](int chi, int t0) {
     // online softmax: entry (head tile, head, frame); 16 lanes per head
 #pragma unroll
     for (int e = 0; e < SMX; ++e) {
@@ -369,7 +356,26 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
       }
     }
   };
-
+  auto step = [&](u32x4v (&buf)[NLD], int chi) {
+    const int t0 = ts + chi * kTc;
+    __syncthreads();  // previous sub-chunk's readers are done with se / sp
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int v = tid + i * kThreads;
+      const int row = v / (ROW / 8), col = v - row * (ROW / 8);
+      if (v < NV) *reinterpret_cast<u32x4v*>(&se[row * RS + col * 8]) = buf[i];
+    }
+    __syncthreads();
+    if (MODE != 2 && chi + PF < nch) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
+    if constexpr (MODE == 1) {  // probe: the load / LDS-write skeleton alone (one LDS read keeps it live)
+      sink += (float)se[(tid * 9) % (kTc * RS)];
+      return;
+    }
+    scores([&](int ks, int p) {
+      return *reinterpret_cast<const half8*>(&se[l16 * RS + p * D + c0 + ks * 32 + 8 * lq]);
+    });
+    tail(chi, t0);
+  };
   u32x4v pre0[NLD];
   u32x4v pre1[PF == 2 ? NLD : 1];
   if (nch > 0) fetch(pre0, 0);

@@ -96,12 +96,19 @@ def main() -> None:
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--decode-only", action="store_true")
+    ap.add_argument("--shape", default=None, help="m,n,k: one prefill-kernel shape only (profiling)")
+    ap.add_argument("--prec", type=int, default=0, help="with --shape: 0 f16x2, 1 f16")
     args = ap.parse_args()
     import torch
 
     rows = []
+    if args.shape:
+        m, n, k = (int(v) for v in args.shape.split(","))
+        rows.append(bench_shape(torch, m, n, k, args.prec, 1, args.iters, graph=not args.no_graph))
+        args.decode_only = True
+        enc_m = []
     enc_m = [1500, 48000] if not args.quick else [1500, 12000]
-    for prec in (wq4.PREC_F16X2, wq4.PREC_F16):
+    for prec in (() if args.shape else (wq4.PREC_F16X2, wq4.PREC_F16)):
         for (n, k) in [(1280, 1280), (3840, 1280), (5120, 1280), (1280, 5120)]:
             for m in ([] if args.decode_only else enc_m):
                 rows.append(bench_shape(torch, m, n, k, prec, 1, args.iters, graph=not args.no_graph))
