@@ -272,7 +272,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
           }
         }
         sacc[ht] = mfma16x32(a[0], b[0], sacc[ht]);
-        if (NS == 2) {
+        if constexpr (NS == 2) {
           sacc[ht] = mfma16x32(a[1], b[0], sacc[ht]);
           sacc[ht] = mfma16x32(a[0], b[1], sacc[ht]);
         }
