@@ -414,26 +414,26 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
 }
 
 // ---------------------------------------- merge + out = Wv Zn + bv --
-// grid (H, ceil(R / 4)), 512 threads: the head's 64 raw Wv rows (46 KB of
-// Q4_0 blocks) and 4 rows of Zn ([column] x 4 rows) in LDS; thread (row pair
-// d, d + 32; blocks b, b + 16, b + 32) dequantizes each block once for the 4
-// rows; 16 block-group partials per output are added through LDS and
-// out[r][h*64 + d] + bv goes into the A-tiled operand of the output
-// projection.
-template <int NS, int WK>
+// grid (H, ceil(R / RPW)), 512 threads: the head's 64 raw Wv rows (46 KB of
+// Q4_0 blocks, LDS-DMA) and RPW rows of Zn ([column][row]) in LDS; thread
+// (row pair d, d + 32; blocks b, b + 16, b + 32) dequantizes each block once
+// for the RPW rows; 16 block-group partials per output are added through LDS
+// and out[r][h*64 + d] + bv goes into the A-tiled operand of the output
+// projection.  Fewer rows per workgroup spread the split-partial stream
+// (S * 5 KB per row and head) over more CUs.
+template <int NS, int WK, int RPW>
 __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict__ zpart,
                                                         const float* __restrict__ mlpart, int R, int H, int D, int S,
                                                         const uint8_t* __restrict__ wv,
                                                         const float* __restrict__ bv, _Float16* __restrict__ tiled) {
   constexpr int kStage = WK == kWtQ4 ? 64 * (kMaxD / 32) * 18 : 16;  // 46 KB of Q4 blocks
   __shared__ __attribute__((aligned(16))) uint8_t sw[kStage];
-  __shared__ __attribute__((aligned(16))) floatx4 zs[kMaxD];  // [column] x 4 rows
-  __shared__ float red[16][64][5];
-  const int h = blockIdx.x, r0 = blockIdx.y * 4, tid = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) float zs[kMaxD * RPW];  // [column][row]
+  __shared__ float red[16][64][RPW + 1];
+  const int h = blockIdx.x, r0 = blockIdx.y * RPW, tid = threadIdx.x;
   const int nkb = D / 32;
   // the value bias of this thread's final outputs, loaded up front
-  const floatx4 bias4 = tid < 64 ? *reinterpret_cast<const floatx4*>(bv + h * 64 + 4 * (tid & 15))
-                                 : floatx4{0.f, 0.f, 0.f, 0.f};
+  const float bias1 = tid < 64 * RPW ? bv[h * 64 + (tid & 63)] : 0.0f;
   const size_t rowbytes = (size_t)nkb * 18;
   if (WK == kWtQ4) {  // the head's 64 rows are contiguous: 64 * nkb * 18 bytes
     const uint8_t* src = wv + (size_t)h * 64 * rowbytes;
@@ -451,8 +451,7 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
   // the merge costs one memory round trip; rows >= R give zeros.
   {
     const int nq = D / 4;
-    float* zsf = reinterpret_cast<float*>(zs);
-    for (int it = tid; it < 4 * nq; it += 512) {
+    for (int it = tid; it < RPW * nq; it += 512) {
       const int j = it / nq, q = it - j * nq;
       const bool rok = r0 + j < R;
       const size_t rb = (size_t)(rok ? r0 + j : 0) * S;
@@ -481,13 +480,18 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
           for (int e = 0; e < 4; ++e) acc[e] = fmaf(w, zv[s][e], acc[e]);
         }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) zsf[(4 * q + e) * 4 + j] = rok ? acc[e] / lsum : 0.0f;
+      for (int e = 0; e < 4; ++e) zs[(4 * q + e) * RPW + j] = rok ? acc[e] / lsum : 0.0f;
     }
   }
   if (WK == kWtQ4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stage pieces landed
   __syncthreads();
   const int dp = tid & 31, bg = tid >> 5;  // rows dp, dp + 32; blocks bg, bg + 16, bg + 32
-  floatx4 acc0{0.0f, 0.0f, 0.0f, 0.0f}, acc1{0.0f, 0.0f, 0.0f, 0.0f};
+  float acc0[RPW], acc1[RPW];
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    acc0[j] = 0.0f;
+    acc1[j] = 0.0f;
+  }
 #pragma unroll 1
   for (int kb = bg; kb < nkb; kb += 16) {
     if (WK == kWtQ4) {
@@ -506,9 +510,9 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
         for (int q = 0; q < 4; ++q) {
           const float wa = (float)((int)((t0 >> sh[q]) & 15u) - 8) * d0;
           const float wb = (float)((int)((t1 >> sh[q]) & 15u) - 8) * d1;
-          const floatx4 z = zs[kb * 32 + e[q]];
+          const float* z = &zs[(kb * 32 + e[q]) * RPW];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < RPW; ++j) {
             acc0[j] = fmaf(wa, z[j], acc0[j]);
             acc1[j] = fmaf(wb, z[j], acc1[j]);
           }
@@ -520,9 +524,9 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
       load_w32<WK>(wv, D, h * 64 + dp + 32, kb, w1);
 #pragma unroll
       for (int i = 0; i < 32; ++i) {
-        const floatx4 z = zs[kb * 32 + i];
+        const float* z = &zs[(kb * 32 + i) * RPW];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < RPW; ++j) {
           acc0[j] = fmaf(w0[i], z[j], acc0[j]);
           acc1[j] = fmaf(w1[i], z[j], acc1[j]);
         }
@@ -530,24 +534,18 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
     }
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < RPW; ++j) {
     red[bg][dp][j] = acc0[j];
     red[bg][dp + 32][j] = acc1[j];
   }
   __syncthreads();
-  if (tid < 64) {
-    const int j = tid >> 4, d0 = 4 * (tid & 15), r = r0 + j;
-    if (r < R) {
-      float o[4];
+  if (tid < 64 * RPW) {  // thread (row j, output d): the block-group sum in group order, then 4-wide stores
+    const int j = tid >> 6, d = tid & 63, r = r0 + j;
+    float sacc = bias1;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float sacc = bias4[i];
-#pragma unroll
-        for (int g = 0; g < 16; ++g) sacc += red[g][d0 + i][j];
-        o[i] = sacc;
-      }
-      atile_store4<NS>(tiled, r, h * 64 + d0, kbp_of(D), o[0], o[1], o[2], o[3]);
-    }
+    for (int g = 0; g < 16; ++g) sacc += red[g][d][j];
+    const float v1 = __shfl_down(sacc, 1, 64), v2 = __shfl_down(sacc, 2, 64), v3 = __shfl_down(sacc, 3, 64);
+    if (r < R && (d & 3) == 0) atile_store4<NS>(tiled, r, h * 64 + d, kbp_of(D), sacc, v1, v2, v3);
   }
 }
 
@@ -604,6 +602,26 @@ void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T,
   } else {
     hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 4, 1>), g, dim3(256), 0, st, qt, enc, Tq, T, H, S, CH, z, ml);
   }
+}
+
+// rows of Zn per xattn_out workgroup (WA_XATTN_OUT_ROWS = 1, 2 or 4)
+int xattn_out_rows() {
+  static const int v = [] {
+    const char* e = getenv("WA_XATTN_OUT_ROWS");
+    const int r = e ? atoi(e) : 4;  // measured: 4 rows beat 1 or 2 (Wv stage shared by more rows)
+    return (r == 1 || r == 2) ? r : 4;
+  }();
+  return v;
+}
+template <int NS, int WK>
+void launch_out(int rpw, dim3 go, const float* z, const float* ml, int R, int H, int D, int S, const uint8_t* wv,
+                const float* bv, _Float16* tiled, hipStream_t st) {
+  if (rpw == 4)
+    hipLaunchKernelGGL((xattn_out_kernel<NS, WK, 4>), go, dim3(512), 0, st, z, ml, R, H, D, S, wv, bv, tiled);
+  else if (rpw == 2)
+    hipLaunchKernelGGL((xattn_out_kernel<NS, WK, 2>), go, dim3(512), 0, st, z, ml, R, H, D, S, wv, bv, tiled);
+  else
+    hipLaunchKernelGGL((xattn_out_kernel<NS, WK, 1>), go, dim3(512), 0, st, z, ml, R, H, D, S, wv, bv, tiled);
 }
 
 }  // namespace
@@ -686,17 +704,18 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   return hipErrorInvalidValue;
 #undef WA_XMAIN
   // merge the splits and project with Wv into the output projection's operand
-  const dim3 go(H, (R + 3) / 4);
+  const int rpw = xattn_out_rows();
+  const dim3 go(H, (R + rpw - 1) / rpw);
   if (wtype == kWtQ4) {
     if (ns == 2)
-      hipLaunchKernelGGL((xattn_out_kernel<2, kWtQ4>), go, dim3(512), 0, st, z, ml, R, H, D, p.splits, wv, bv, tiled);
+      launch_out<2, kWtQ4>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
     else
-      hipLaunchKernelGGL((xattn_out_kernel<1, kWtQ4>), go, dim3(512), 0, st, z, ml, R, H, D, p.splits, wv, bv, tiled);
+      launch_out<1, kWtQ4>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
   } else {
     if (ns == 2)
-      hipLaunchKernelGGL((xattn_out_kernel<2, kWtF16>), go, dim3(512), 0, st, z, ml, R, H, D, p.splits, wv, bv, tiled);
+      launch_out<2, kWtF16>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
     else
-      hipLaunchKernelGGL((xattn_out_kernel<1, kWtF16>), go, dim3(512), 0, st, z, ml, R, H, D, p.splits, wv, bv, tiled);
+      launch_out<1, kWtF16>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
   }
   return hipGetLastError();
 }
