@@ -835,6 +835,70 @@ __device__ __forceinline__ void better_pair(float& bv, int& bi, float v, int i) 
   }
 }
 
+// Greedy pick of a workgroup's 32 x 128 logits block lg[clip][kLgPickLd]
+// (already masked), then the last-arriving workgroup's pick over all
+// workgroups' candidates (see logits_argmax_kernel).
+constexpr int kLgPickLd = 132;
+__device__ __forceinline__ void pick_from_lds(const float* lg, int B, int V, float* __restrict__ pval,
+                                              int* __restrict__ pidx, int* __restrict__ counter,
+                                              int* __restrict__ out_tok, int* ticket) {
+  const int tid = threadIdx.x, nwg = gridDim.x;
+  __syncthreads();
+  const int row = tid >> 3, part = tid & 7;
+  float bv = -INFINITY;
+  int bi = -1;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int c = part * 16 + j;
+    const int idx = blockIdx.x * 128 + c;
+    if (idx < V) better_pair(bv, bi, lg[row * kLgPickLd + c], idx);
+  }
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    const float v2 = __shfl_xor(bv, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    better_pair(bv, bi, v2, i2);
+  }
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(pval, 0, 32 * nwg * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(pidx, 0, 32 * nwg * 4, 0x00020000);
+  if (part == 0 && row < B) {
+    const uint32_t off = (uint32_t)(row * nwg + blockIdx.x) * 4;
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bv), rv, off, 0, 16);  // sc1
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)bi, ri, off, 0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    typedef __attribute__((address_space(1))) int gint;
+    const int prev = __hip_atomic_fetch_add((gint*)counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *ticket = prev == nwg - 1;
+  }
+  __syncthreads();
+  if (!*ticket) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: loads stay below the ticket
+  bv = -INFINITY;
+  bi = -1;
+  if (row < B) {
+    for (int j = part; j < nwg; j += 8) {
+      const uint32_t off = (uint32_t)(row * nwg + j) * 4;
+      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, off, 0, 16));
+      const int i = (int)__builtin_amdgcn_raw_buffer_load_b32(ri, off, 0, 16);
+      better_pair(bv, bi, v, i);
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    const float v2 = __shfl_xor(bv, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    better_pair(bv, bi, v2, i2);
+  }
+  if (part == 0 && row < B) out_tok[row] = bi < 0 ? 0 : bi;
+  if (tid == 0) {
+    typedef __attribute__((address_space(1))) int gint;
+    __hip_atomic_store((gint*)counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  }
+}
+
 __global__ __launch_bounds__(256) void logits_argmax_kernel(const float* __restrict__ hid, int B, int D, long ldh,
                                                             const float* __restrict__ emb, int V, int min_tokens,
                                                             const DecodeState* __restrict__ state,
@@ -844,7 +908,6 @@ __global__ __launch_bounds__(256) void logits_argmax_kernel(const float* __restr
   __shared__ int ticket;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int nwg = gridDim.x;
   const int n = blockIdx.x * 128 + wave * 32 + r;
   const float* er = emb + (size_t)(n < V ? n : V - 1) * D;
   const int nch = (D + kLgChunk - 1) / kLgChunk;
@@ -886,79 +949,127 @@ __global__ __launch_bounds__(256) void logits_argmax_kernel(const float* __restr
   // this workgroup's 32 x 128 logits -> LDS, then (max, index) per clip
   __syncthreads();
   float* lg = hs;  // [32 rows][128 + 4]
-  constexpr int kLd = 132;
   const int suppress = state->step + 1 < min_tokens;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
     float v = acc[i];
     if (n >= V || (suppress && n == kEOT)) v = -INFINITY;
-    lg[row * kLd + wave * 32 + r] = v;
+    lg[row * kLgPickLd + wave * 32 + r] = v;
   }
-  __syncthreads();
-  const int row = tid >> 3, part = tid & 7;
-  float bv = -INFINITY;
-  int bi = -1;
+  pick_from_lds(lg, B, V, pval, pidx, counter, out_tok, &ticket);
+}
+
+// The same on f16 MFMA: the embedding as exact-to-2^-22 f16 pairs
+// (emb2 [V][NS][D], launch_enc_planes of the f32 table, prepared once),
+// E = hi + lo, and the hidden rows split likewise; three 32x32x16 f16
+// MFMAs per product (hi*hi + lo*hi + hi*lo) with f32 accumulation, 16x
+// the f32 MFMA rate, so the 265 MB table streams at HBM speed.  Workgroup =
+// 4 waves x 32 vocabulary rows (m), the 32 clips as n; per 128-dim chunk
+// the hidden rows are staged in LDS as f16 pairs and the next chunk's
+// embedding fragments are already in flight in registers.
+constexpr int kLg2Chunk = 128;
+constexpr int kLg2Ld = kLg2Chunk + 8;  // halves
+
+template <int NS>
+__global__ __launch_bounds__(256) void logits_argmax_f16_kernel(const float* __restrict__ hid, int B, int D, long ldh,
+                                                                const _Float16* __restrict__ emb2, int V,
+                                                                int min_tokens, const DecodeState* __restrict__ state,
+                                                                float* __restrict__ pval, int* __restrict__ pidx,
+                                                                int* __restrict__ counter, int* __restrict__ out_tok) {
+  __shared__ __attribute__((aligned(16))) _Float16 hsh[NS][32 * kLg2Ld];
+  __shared__ __attribute__((aligned(16))) float lg[32 * kLgPickLd];
+  __shared__ int ticket;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, lh = lane >> 5;
+  const int v0 = blockIdx.x * 128 + wave * 32;
+  const int vrow = v0 + r < V ? v0 + r : V - 1;
+  const _Float16* er = emb2 + (size_t)vrow * NS * D;
+  const int nch = (D + kLg2Chunk - 1) / kLg2Chunk;
+  constexpr int KS = kLg2Chunk / 16;
+  floatx16 acc;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int c = part * 16 + j;
-    const int idx = blockIdx.x * 128 + c;
-    if (idx < V) better_pair(bv, bi, lg[row * kLd + c], idx);
-  }
+  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+  half8 ec[KS][NS], en[KS][NS];
+  auto load_e = [&](half8 (&e)[KS][NS], int kc) {
 #pragma unroll
-  for (int o = 1; o < 8; o <<= 1) {
-    const float v2 = __shfl_xor(bv, o, 64);
-    const int i2 = __shfl_xor(bi, o, 64);
-    better_pair(bv, bi, v2, i2);
-  }
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(pval, 0, 32 * nwg * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(pidx, 0, 32 * nwg * 4, 0x00020000);
-  if (part == 0 && row < B) {
-    const uint32_t off = (uint32_t)(row * nwg + blockIdx.x) * 4;
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bv), rv, off, 0, 16);  // sc1
-    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)bi, ri, off, 0, 16);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    typedef __attribute__((address_space(1))) int gint;
-    const int prev = __hip_atomic_fetch_add((gint*)counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ticket = prev == nwg - 1;
-  }
-  __syncthreads();
-  if (!ticket) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: loads stay below the ticket
-  bv = -INFINITY;
-  bi = -1;
-  if (row < B) {
-    for (int j = part; j < nwg; j += 8) {
-      const uint32_t off = (uint32_t)(row * nwg + j) * 4;
-      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, off, 0, 16));
-      const int i = (int)__builtin_amdgcn_raw_buffer_load_b32(ri, off, 0, 16);
-      better_pair(bv, bi, v, i);
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int p = 0; p < NS; ++p) {
+        const int k = kc + 16 * ks + 8 * lh;
+        e[ks][p] = *reinterpret_cast<const half8*>(er + (size_t)p * D + (k < D ? k : 0));
+      }
+  };
+  load_e(ec, 0);
+  for (int c = 0; c < nch; ++c) {
+    const int kc = c * kLg2Chunk;
+    if (c + 1 < nch) load_e(en, kc + kLg2Chunk);
+    __syncthreads();
+    for (int e = tid; e < 32 * (kLg2Chunk / 4); e += 256) {  // (row, 4 dims) -> f16 pairs
+      const int row = e / (kLg2Chunk / 4), k4 = (e % (kLg2Chunk / 4)) * 4;
+      const floatx4 x = (row < B && kc + k4 < D) ? *reinterpret_cast<const floatx4*>(hid + (size_t)row * ldh + kc + k4)
+                                                 : floatx4{0.f, 0.f, 0.f, 0.f};
+      ea_half4 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        _Float16 a, b;
+        split_f16(x[j], a, b);
+        hi[j] = a;
+        lo[j] = b;
+      }
+      *reinterpret_cast<ea_half4*>(&hsh[0][row * kLg2Ld + k4]) = hi;
+      if constexpr (NS == 2) *reinterpret_cast<ea_half4*>(&hsh[NS - 1][row * kLg2Ld + k4]) = lo;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bool kin = kc + 16 * ks < D;  // D % 16 == 0
+      if (kin) {
+        const half8 bh = *reinterpret_cast<const half8*>(&hsh[0][r * kLg2Ld + 16 * ks + 8 * lh]);
+        acc = ea_mfma(ec[ks][0], bh, acc);
+        if constexpr (NS == 2) {
+          const half8 bl = *reinterpret_cast<const half8*>(&hsh[1][r * kLg2Ld + 16 * ks + 8 * lh]);
+          acc = ea_mfma(ec[ks][1], bh, acc);
+          acc = ea_mfma(ec[ks][0], bl, acc);
+        }
+      }
+    }
+    if (c + 1 < nch) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int p = 0; p < NS; ++p) ec[ks][p] = en[ks][p];
     }
   }
+  // acc: m = vocab v0 + row(i), n = clip r -> lg[clip][vocab]
+  const int suppress = state->step + 1 < min_tokens;
 #pragma unroll
-  for (int o = 1; o < 8; o <<= 1) {
-    const float v2 = __shfl_xor(bv, o, 64);
-    const int i2 = __shfl_xor(bi, o, 64);
-    better_pair(bv, bi, v2, i2);
+  for (int i = 0; i < 16; ++i) {
+    const int vl = (i & 3) + 8 * (i >> 2) + 4 * lh;
+    const int n = v0 + vl;
+    float v = acc[i];
+    if (n >= V || (suppress && n == kEOT)) v = -INFINITY;
+    lg[r * kLgPickLd + wave * 32 + vl] = v;
   }
-  if (part == 0 && row < B) out_tok[row] = bi < 0 ? 0 : bi;
-  if (tid == 0) {
-    typedef __attribute__((address_space(1))) int gint;
-    __hip_atomic_store((gint*)counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-  }
+  pick_from_lds(lg, B, V, pval, pidx, counter, out_tok, &ticket);
 }
 
 int logits_argmax_groups(int V) { return (V + 127) / 128; }
 
-hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const float* emb, int V, int min_tokens,
-                                const DecodeState* state, float* pval, int* pidx, int* counter, int* out_tok,
-                                hipStream_t st) {
-  if (B < 1 || B > 32 || D % 8 != 0 || !state) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(logits_argmax_kernel, dim3(logits_argmax_groups(V)), dim3(256), 0, st, h, B, D, ldh, emb, V,
-                     min_tokens, state, pval, pidx, counter, out_tok);
+hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const float* emb, const _Float16* emb2,
+                                int ns, int V, int min_tokens, const DecodeState* state, float* pval, int* pidx,
+                                int* counter, int* out_tok, hipStream_t st) {
+  if (B < 1 || B > 32 || D % 16 != 0 || !state) return hipErrorInvalidValue;
+  const dim3 grid(logits_argmax_groups(V));
+  if (emb2 && ns == 2)
+    hipLaunchKernelGGL(logits_argmax_f16_kernel<2>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens, state,
+                       pval, pidx, counter, out_tok);
+  else if (emb2)
+    hipLaunchKernelGGL(logits_argmax_f16_kernel<1>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens, state,
+                       pval, pidx, counter, out_tok);
+  else
+    hipLaunchKernelGGL(logits_argmax_kernel, grid, dim3(256), 0, st, h, B, D, ldh, emb, V, min_tokens, state, pval,
+                       pidx, counter, out_tok);
   return hipGetLastError();
 }
 

@@ -87,9 +87,11 @@ hipError_t launch_argmax(const float* logits, int B, int V, int lo, int hi, int 
 // D % 8 == 0; pval / pidx: 32 * logits_argmax_groups(V) scratch each,
 // counter: one int zeroed once (re-armed by the kernel).
 int logits_argmax_groups(int V);
-hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const float* emb, int V, int min_tokens,
-                                const DecodeState* state, float* pval, int* pidx, int* counter, int* out_tok,
-                                hipStream_t st);
+// emb2 != nullptr: the f16-pair table [V][ns][D] (launch_enc_planes of emb)
+// on f16 MFMA; else the f32 table on f32 MFMA.  D % 16 == 0.
+hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const float* emb, const _Float16* emb2,
+                                int ns, int V, int min_tokens, const DecodeState* state, float* pval, int* pidx,
+                                int* counter, int* out_tok, hipStream_t st);
 
 // Greedy-loop bookkeeping at the top of each step (whisper.rs:104-115):
 // for every clip not yet done, EOT -> done (eot_stop != 0), else append the

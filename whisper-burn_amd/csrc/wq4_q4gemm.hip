@@ -846,11 +846,18 @@ DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal) {
     const char* env = getenv("WQ4_DECODE_W8");  // tuning knob (tools/q4_bench.py)
     return env ? atoi(env) != 0 : true;
   }();
-  if (w8 && nbp <= 8 * kDecodeMaxPer8 * kDecodeMaxKs && ntiles <= kDecodeMaxTiles) {
+  // block pairs per wave of the 8-wave plan before K is split over
+  // workgroups (tuning knob WQ4_DECODE_PER8: fewer = more, smaller slices)
+  static const int per8 = [] {
+    const char* env = getenv("WQ4_DECODE_PER8");
+    const int v = env ? atoi(env) : kDecodeMaxPer8;
+    return v >= 1 && v <= kDecodeMaxPer8 ? v : kDecodeMaxPer8;
+  }();
+  if (w8 && nbp <= 8 * per8 * kDecodeMaxKs && ntiles <= kDecodeMaxTiles) {
     // larger K: the same 8-wave workgroups over ks K slices (sc1 slabs +
     // last-arriver merge); ks depends on K only
     p.w = 8;
-    p.ks = (int)((nbp + 8 * kDecodeMaxPer8 - 1) / (8 * kDecodeMaxPer8));
+    p.ks = (int)((nbp + 8 * per8 - 1) / (8 * per8));
     while (p.ks > 1 && ntiles * p.ks * 1024 > (int64_t)kDecodeWsFloats) --p.ks;  // workspace bound
     p.chunk = (int)((nbp + 8 * p.ks - 1) / (8 * p.ks));
     p.per = p.chunk;
