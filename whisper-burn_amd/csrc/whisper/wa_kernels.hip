@@ -171,6 +171,7 @@ __device__ __forceinline__ floatx16 ea_mfma(half8 a, half8 b, floatx16 c) {
 }
 
 constexpr int kEaKeys = 64;  // keys per LDS tile
+constexpr float kEaQScale = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
 constexpr int kEaLd = 72;    // LDS row stride (halves)
 
 template <int NS>
@@ -196,7 +197,9 @@ __global__ __launch_bounds__(256) void encoder_attention_f16_kernel(const float*
       half8 hi, lo;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float v = q < T ? (j < 4 ? x0[j] : x1[j - 4]) * 0.125f : 0.0f;
+        // q / 8 * log2(e): the scores come out in base-2 units, so the
+        // softmax exponentials are single v_exp_f32 (2^x) instructions
+        const float v = q < T ? (j < 4 ? x0[j] : x1[j - 4]) * kEaQScale : 0.0f;
         _Float16 a, c;
         split_f16(v, a, c);
         hi[j] = a;
@@ -288,11 +291,11 @@ __global__ __launch_bounds__(256) void encoder_attention_f16_kernel(const float*
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m, mx);
-      const float alpha = expf(m - mn);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);  // exp2(-inf) = 0
       float rs = 0.0f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        st[i] = expf(st[i] - mn);
+        st[i] = __builtin_amdgcn_exp2f(st[i] - mn);
         rs += st[i];
       }
       rs += __shfl_xor(rs, 32, 64);
