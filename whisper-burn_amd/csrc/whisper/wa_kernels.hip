@@ -27,6 +27,9 @@ using wq4::floatx4;
 using wq4::half8;
 
 constexpr int kEOT = 50257;
+// attention scores scaled by 1/sqrt(64) * log2(e) (attention.rs:262): the
+// softmax runs in base 2, one v_exp_f32 (2^x) per exponential
+constexpr float kEaQScale = 0.125f * 1.4426950408889634f;
 
 using wq4::kLnMaxV;
 using wq4::wave_sum;
@@ -171,7 +174,6 @@ __device__ __forceinline__ floatx16 ea_mfma(half8 a, half8 b, floatx16 c) {
 }
 
 constexpr int kEaKeys = 64;  // keys per LDS tile
-constexpr float kEaQScale = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
 constexpr int kEaLd = 72;    // LDS row stride (halves)
 
 template <int NS>
@@ -410,8 +412,8 @@ __device__ __forceinline__ void attn_scan(const floatx4 (&qv)[TQ], int Tq, int k
           for (int off = 1; off < 16; off <<= 1) dot += __shfl_xor(dot, off, 64);
           if (j < k1 && vis(t, j)) {
             const float mn = fmaxf(m[t], dot);
-            const float alpha = expf(m[t] - mn);
-            const float p = expf(dot - mn);
+            const float alpha = __builtin_amdgcn_exp2f(m[t] - mn);  // base-2 units
+            const float p = __builtin_amdgcn_exp2f(dot - mn);
             l[t] = l[t] * alpha + p;
             o[t] = o[t] * alpha + vv[u] * p;
             m[t] = mn;
@@ -439,8 +441,8 @@ __device__ __forceinline__ void attn_merge(int Tq, int wave, int lane, float (&m
 #pragma unroll
       for (int e = 0; e < 4; ++e) o2[e] = __shfl_xor(o[t][e], off, 64);
       const float mx = fmaxf(m[t], m2);
-      const float a1 = m[t] == -INFINITY ? 0.0f : expf(m[t] - mx);
-      const float a2 = m2 == -INFINITY ? 0.0f : expf(m2 - mx);
+      const float a1 = m[t] == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(m[t] - mx);
+      const float a2 = m2 == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(m2 - mx);
       l[t] = l[t] * a1 + l2 * a2;
       o[t] = o[t] * a1 + o2 * a2;
       m[t] = mx;
@@ -464,7 +466,7 @@ __device__ __forceinline__ void attn_merge(int Tq, int wave, int lane, float (&m
     for (int w = 0; w < 4; ++w) mn = fmaxf(mn, wm[w][t]);
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      const float a = wm[w][t] == -INFINITY ? 0.0f : expf(wm[w][t] - mn);
+      const float a = wm[w][t] == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(wm[w][t] - mn);
       ls += wl[w][t] * a;
       os += wo[w][t][lane] * a;
     }
@@ -504,7 +506,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
 #pragma unroll
   for (int t = 0; t < TQ; ++t)
     qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + sub * 4) *
-                         0.125f
+                         kEaQScale
                    : floatx4{0.f, 0.f, 0.f, 0.f};
   const int nk = kv_len + Tq;
   const int per_wave = (nk + 3) / 4;

@@ -138,7 +138,9 @@ __global__ __launch_bounds__(256) void xattn_q_kernel(const float* __restrict__ 
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       _Float16 x, y;
-      split_f16(acc[i] * 0.125f, x, y);  // / sqrt(64) (attention.rs:262), exact
+      // / sqrt(64) (attention.rs:262) * log2(e): scores in base-2 units, so
+      // the softmax uses v_exp_f32 (2^x) directly
+      split_f16(acc[i] * (0.125f * 1.4426950408889634f), x, y);
       hi[i] = x;
       lo[i] = y;
     }
@@ -305,8 +307,8 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
         const float mn = fmaxf(M[e], cm);
         float alpha = 1.0f, p = 0.0f;
         if (mn != -INFINITY) {
-          alpha = expf(M[e] - mn);
-          p = valid ? expf(sv - mn) : 0.0f;
+          alpha = __builtin_amdgcn_exp2f(M[e] - mn);
+          p = valid ? __builtin_amdgcn_exp2f(sv - mn) : 0.0f;
         }
         float ps = p;
 #pragma unroll
@@ -474,7 +476,7 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
 #pragma unroll
       for (int s = 0; s < kMaxSplits; ++s)
         if (s < S) {
-          const float w = ml[s][0] == -INFINITY ? 0.0f : expf(ml[s][0] - mx);
+          const float w = ml[s][0] == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(ml[s][0] - mx);  // base-2 units
           lsum = fmaf(w, ml[s][1], lsum);
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc[e] = fmaf(w, zv[s][e], acc[e]);
