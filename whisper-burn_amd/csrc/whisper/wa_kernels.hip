@@ -1059,6 +1059,137 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_kernel(const float* __r
   pick_from_lds(lg, B, V, pval, pidx, counter, out_tok, &ticket);
 }
 
+// 16x16x32 form of logits_argmax_f16_kernel: a lane's embedding fragment
+// is 8 dims of one of 16 rows, so one load instruction covers 16 rows x 64
+// contiguous bytes (the 32x32x16 form: 32 rows x 32 B) -- half the rows
+// touched per instruction for the same bytes.  Wave = 32 vocabulary rows as
+// two 16-row m-tiles, the 32 clips as two n-tiles.
+template <int NS>
+__global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
+    const float* __restrict__ hid, int B, int D, long ldh, const _Float16* __restrict__ emb2, int V, int min_tokens,
+    const DecodeState* __restrict__ state, float* __restrict__ pval, int* __restrict__ pidx, int* __restrict__ counter,
+    int* __restrict__ out_tok) {
+  __shared__ __attribute__((aligned(16))) _Float16 hsh[NS][32 * kLg2Ld];
+  __shared__ __attribute__((aligned(16))) float lg[32 * kLgPickLd];
+  __shared__ int ticket;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l16 = lane & 15, lq = lane >> 4;
+  const int v0 = blockIdx.x * 128 + wave * 32;
+  const _Float16* er[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int v = v0 + 16 * mt + l16;
+    er[mt] = emb2 + (size_t)(v < V ? v : V - 1) * NS * D;
+  }
+  const int nch = (D + kLg2Chunk - 1) / kLg2Chunk;
+  constexpr int KS = kLg2Chunk / 32;
+  floatx4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+  half8 ec[2][KS][NS], en[2][KS][NS];
+  auto load_e = [&](half8 (&e)[2][KS][NS], int kc) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int p = 0; p < NS; ++p) {
+          const int k = kc + 32 * ks + 8 * lq;
+          e[mt][ks][p] = *reinterpret_cast<const half8*>(er[mt] + (size_t)p * D + (k < D ? k : 0));
+        }
+  };
+  // the hidden rows of a chunk (f32, thread: row e / 32, 4 dims) travel one
+  // chunk ahead in registers too, so no chunk waits on a dependent load
+  constexpr int HPT = 32 * kLg2Chunk / 4 / 256;  // float4s per thread per chunk
+  floatx4 hc[HPT], hn[HPT];
+  // branch-free (clamped address, select after the load): the loads of a
+  // chunk form one straight-line group, so the compiler's vmcnt waits before
+  // the next chunk's use can leave the prefetched chunk in flight
+  auto load_h = [&](floatx4 (&hv)[HPT], int kc) {
+#pragma unroll
+    for (int i = 0; i < HPT; ++i) {
+      const int e = tid + 256 * i;
+      const int row = e / (kLg2Chunk / 4), k4 = (e % (kLg2Chunk / 4)) * 4;
+      const bool ok = row < B && kc + k4 < D;
+      const floatx4 v = *reinterpret_cast<const floatx4*>(hid + (size_t)(row < B ? row : 0) * ldh +
+                                                          (kc + k4 < D ? kc + k4 : 0));
+      hv[i] = ok ? v : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  load_e(ec, 0);
+  load_h(hc, 0);
+  for (int c = 0; c < nch; ++c) {
+    const int kc = c * kLg2Chunk;
+    {  // the last chunk re-loads itself: no conditional load group
+      const int kn = c + 1 < nch ? kc + kLg2Chunk : kc;
+      load_e(en, kn);
+      load_h(hn, kn);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < HPT; ++i) {  // (row, 4 dims) -> f16 pairs
+      const int e = tid + 256 * i;
+      const int row = e / (kLg2Chunk / 4), k4 = (e % (kLg2Chunk / 4)) * 4;
+      ea_half4 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        _Float16 a, b;
+        split_f16(hc[i][j], a, b);
+        hi[j] = a;
+        lo[j] = b;
+      }
+      *reinterpret_cast<ea_half4*>(&hsh[0][row * kLg2Ld + k4]) = hi;
+      if constexpr (NS == 2) *reinterpret_cast<ea_half4*>(&hsh[NS - 1][row * kLg2Ld + k4]) = lo;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {  // D % kLg2Chunk == 0 (launcher): no partial chunk
+      {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int off = (16 * nt + l16) * kLg2Ld + 32 * ks + 8 * lq;
+          const half8 bh = *reinterpret_cast<const half8*>(&hsh[0][off]);
+          half8 bl;
+          if constexpr (NS == 2) bl = *reinterpret_cast<const half8*>(&hsh[1][off]);
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ec[mt][ks][0], bh, acc[mt][nt], 0, 0, 0);
+            if constexpr (NS == 2) {
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ec[mt][ks][1], bh, acc[mt][nt], 0, 0, 0);
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ec[mt][ks][0], bl, acc[mt][nt], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int p = 0; p < NS; ++p) ec[mt][ks][p] = en[mt][ks][p];
+#pragma unroll
+    for (int i = 0; i < HPT; ++i) hc[i] = hn[i];
+  }
+  // acc[mt][nt]: lane holds clip 16 nt + l16, vocab v0 + 16 mt + 4 lq + j
+  const int suppress = state->step + 1 < min_tokens;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int vl = 16 * mt + 4 * lq + j;
+        const int n = v0 + vl;
+        float v = acc[mt][nt][j];
+        if (n >= V || (suppress && n == kEOT)) v = -INFINITY;
+        lg[(16 * nt + l16) * kLgPickLd + wave * 32 + vl] = v;
+      }
+  pick_from_lds(lg, B, V, pval, pidx, counter, out_tok, &ticket);
+}
+
 int logits_argmax_groups(int V) { return (V + 127) / 128; }
 
 hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const float* emb, const _Float16* emb2,
@@ -1066,7 +1197,14 @@ hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const fl
                                 int* counter, int* out_tok, hipStream_t st) {
   if (B < 1 || B > 32 || D % 16 != 0 || !state) return hipErrorInvalidValue;
   const dim3 grid(logits_argmax_groups(V));
-  if (emb2 && ns == 2)
+  static const bool k32 = [] {  // WA_LOGITS_K32=0: the 32x32x16 form (A/B)
+    const char* e = getenv("WA_LOGITS_K32");
+    return e ? atoi(e) != 0 : true;
+  }();
+  if (emb2 && ns == 2 && k32 && D % kLg2Chunk == 0)
+    hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<2>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens,
+                       state, pval, pidx, counter, out_tok);
+  else if (emb2 && ns == 2)
     hipLaunchKernelGGL(logits_argmax_f16_kernel<2>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens, state,
                        pval, pidx, counter, out_tok);
   else if (emb2)
