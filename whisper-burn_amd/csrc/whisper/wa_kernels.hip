@@ -632,13 +632,137 @@ __global__ __launch_bounds__(256) void conv_gelu_kernel(const float* __restrict_
       }
 }
 
+// The same conv1d + GELU (+ positional add) on f16 MFMA: A (im2col rows)
+// and B (weights [N][3C]) staged per 32-k step as exact-to-2^-22 f16 pairs,
+// v_mfma_f32_32x32x16_f16 with three products per term (the arithmetic of the
+// Q4 GEMMs).  Thread stages 4 consecutive k of one row: one float4 load when
+// the input is channel-contiguous (conv2: in_cs == 1), four scalars
+// otherwise (conv1 reads the mel [n_mels][3000] layout).  LDS row stride 40
+// halves: conflict-free b128 fragment reads.
+constexpr int kCvLd = 40;
+template <int NS>
+__global__ __launch_bounds__(256) void conv_gelu_f16_kernel(const float* __restrict__ in, long in_bs, long in_cs,
+                                                            long in_ts, int B, int C, int T_in, int S,
+                                                            const float* __restrict__ wt,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ pos, int N,
+                                                            float* __restrict__ out, int T_out) {
+  __shared__ __attribute__((aligned(16))) _Float16 as[NS][128 * kCvLd];
+  __shared__ __attribute__((aligned(16))) _Float16 bs[NS][128 * kCvLd];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, lh = lane >> 5;
+  const int M = B * T_out, K = 3 * C;
+  const int m0 = blockIdx.x * 128, n0 = blockIdx.y * 128;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][c][i] = 0.0f;
+  auto put = [&](_Float16 (&dst)[NS][128 * kCvLd], int row, int kl, floatx4 v) {
+    ea_half4 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      _Float16 a, b;
+      split_f16(v[j], a, b);
+      hi[j] = a;
+      lo[j] = b;
+    }
+    *reinterpret_cast<ea_half4*>(&dst[0][row * kCvLd + kl]) = hi;
+    if constexpr (NS == 2) *reinterpret_cast<ea_half4*>(&dst[NS - 1][row * kCvLd + kl]) = lo;
+  };
+  for (int kc = 0; kc < K; kc += 32) {
+    // stage A (im2col gather) and B: 128 rows x 32 k each, (row, 4 k) per item
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int e = it * 256 + tid;
+      const int ml = e >> 3, kl = (e & 7) * 4;
+      const int m = m0 + ml, k = kc + kl;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (m < M && k < K) {
+        const int bb = m / T_out, t = m - bb * T_out;
+        if (in_cs == 1) {  // 4 consecutive channels of one tap (C % 4 == 0)
+          const int kk = k / C, c = k - kk * C;
+          const int ti = t * S + kk - 1;
+          if (ti >= 0 && ti < T_in) v = *reinterpret_cast<const floatx4*>(in + bb * in_bs + c + (long)ti * in_ts);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int kj = k + j, kk = kj / C, c = kj - kk * C;
+            const int ti = t * S + kk - 1;
+            if (kj < K && ti >= 0 && ti < T_in) v[j] = in[bb * in_bs + c * in_cs + (long)ti * in_ts];
+          }
+        }
+      }
+      put(as, ml, kl, v);
+    }
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int e = it * 256 + tid;
+      const int nl = e >> 3, kl = (e & 7) * 4;
+      const int n = n0 + nl, k = kc + kl;
+      const floatx4 v = (n < N && k + 3 < K) ? *reinterpret_cast<const floatx4*>(wt + (size_t)n * K + k)
+                                             : floatx4{0.f, 0.f, 0.f, 0.f};
+      put(bs, nl, kl, v);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k16 = 0; k16 < 2; ++k16) {
+      half8 a[2][NS], b[2][NS];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int p = 0; p < NS; ++p) {
+          a[i][p] = *reinterpret_cast<const half8*>(&as[p][(wm + 32 * i + l32) * kCvLd + 16 * k16 + 8 * lh]);
+          b[i][p] = *reinterpret_cast<const half8*>(&bs[p][(wn + 32 * i + l32) * kCvLd + 16 * k16 + 8 * lh]);
+        }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = ea_mfma(a[i][0], b[j][0], acc[i][j]);
+          if constexpr (NS == 2) {
+            acc[i][j] = ea_mfma(a[i][1], b[j][0], acc[i][j]);
+            acc[i][j] = ea_mfma(a[i][0], b[j][1], acc[i][j]);
+          }
+        }
+    }
+    __syncthreads();
+  }
+  // acc[i][j]: A = rows (m), B = cols (n): lane holds column n = l32, rows (r & 3) + 8 (r >> 2) + 4 lh
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = m0 + wm + 32 * a + (i & 3) + 8 * (i >> 2) + 4 * lh;
+        const int n = n0 + wn + 32 * c + l32;
+        if (m < M && n < N) {
+          float v = wq4::gelu_tanh(acc[a][c][i] + bias[n]);
+          if (pos) v = v + pos[(size_t)(m % T_out) * N + n];
+          out[(size_t)m * N + n] = v;
+        }
+      }
+}
+
 hipError_t launch_conv_gelu(const float* in, long in_bs, long in_cs, long in_ts, int B, int C, int T_in,
                             int stride, const float* w_t, const float* bias, const float* pos, int N, float* out,
                             hipStream_t st) {
   const int T_out = (T_in + 2 - 3) / stride + 1;
   const dim3 grid((B * T_out + 127) / 128, (N + 127) / 128), block(256);
-  hipLaunchKernelGGL(conv_gelu_kernel, grid, block, 0, st, in, in_bs, in_cs, in_ts, B, C, T_in, stride, w_t, bias,
-                     pos, N, out, T_out);
+  static const bool f32_mfma = [] {  // WA_CONV_F32=1: the f32-MFMA kernel (A/B, diagnostics)
+    const char* e = getenv("WA_CONV_F32");
+    return e && atoi(e) != 0;
+  }();
+  if (f32_mfma || C % 4 != 0 || (3 * C) % 4 != 0)
+    hipLaunchKernelGGL(conv_gelu_kernel, grid, block, 0, st, in, in_bs, in_cs, in_ts, B, C, T_in, stride, w_t, bias,
+                       pos, N, out, T_out);
+  else
+    hipLaunchKernelGGL(conv_gelu_f16_kernel<2>, grid, block, 0, st, in, in_bs, in_cs, in_ts, B, C, T_in, stride, w_t,
+                       bias, pos, N, out, T_out);
   return hipGetLastError();
 }
 
