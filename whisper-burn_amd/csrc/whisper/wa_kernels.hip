@@ -176,8 +176,8 @@ __device__ __forceinline__ floatx16 ea_mfma(half8 a, half8 b, floatx16 c) {
 constexpr int kEaKeys = 64;  // keys per LDS tile
 constexpr int kEaLd = 72;    // LDS row stride (halves)
 
-template <int NS>
-__global__ __launch_bounds__(256) void encoder_attention_f16_kernel(const float* __restrict__ qkv, int T, int H,
+template <int NS, int NW>
+__global__ __launch_bounds__(64 * NW) void encoder_attention_f16_kernel(const float* __restrict__ qkv, int T, int H,
                                                                     _Float16* __restrict__ tiled) {
   __shared__ __attribute__((aligned(16))) _Float16 kls[NS][kEaKeys * kEaLd];
   __shared__ __attribute__((aligned(16))) _Float16 vls[NS][kEaKeys * kEaLd];
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void encoder_attention_f16_kernel(const float*
   const int head = blockIdx.y, b = blockIdx.z;
   const int D = H * 64, ld = 3 * D;
   const float* base = qkv + (size_t)b * T * ld;
-  const int q = blockIdx.x * 128 + wave * 32 + l32;
+  const int q = blockIdx.x * (32 * NW) + wave * 32 + l32;
 
   // Q^T operand (k = dim, n = query): lane (query l32, dims 16 ks + 8 lh + 0..7), scaled by 1/8 (exact)
   half8 qb[4][NS];
@@ -211,23 +211,25 @@ __global__ __launch_bounds__(256) void encoder_attention_f16_kernel(const float*
       if constexpr (NS == 2) qb[ks][1] = lo;
     }
   }
-  // staging: thread (key tid / 4, dims 16 (tid % 4) + 0..15) of K and V
-  const int skey = tid >> 2, sd = (tid & 3) * 16;
-  floatx4 kreg[4], vreg[4];
+  // staging: thread (key tid / TPK, dims EPT (tid % TPK) + 0..EPT-1) of K and V
+  constexpr int EPT = 64 * kEaKeys / (64 * NW);  // elements per thread and tensor (16 or 8)
+  constexpr int TPK = 64 / EPT;                  // threads per key
+  const int skey = tid / TPK, sd = (tid % TPK) * EPT;
+  floatx4 kreg[EPT / 4], vreg[EPT / 4];
   auto fetch = [&](int key0) {
     const int key = key0 + skey;
     const bool ok = key < T;
     const float* kr = base + (size_t)(ok ? key : 0) * ld + D + head * 64 + sd;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < EPT / 4; ++i) {
       kreg[i] = ok ? *reinterpret_cast<const floatx4*>(kr + 4 * i) : floatx4{0.f, 0.f, 0.f, 0.f};
       vreg[i] = ok ? *reinterpret_cast<const floatx4*>(kr + D + 4 * i) : floatx4{0.f, 0.f, 0.f, 0.f};
     }
   };
   auto stage = [&]() {
-    half8 kh[2], kl[2], vh[2], vl[2];
+    half8 kh[EPT / 8], kl[EPT / 8], vh[EPT / 8], vl[EPT / 8];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < EPT; ++i) {
       _Float16 a, c;
       split_f16(kreg[i >> 2][i & 3], a, c);
       kh[i >> 3][i & 7] = a;
@@ -237,7 +239,7 @@ __global__ __launch_bounds__(256) void encoder_attention_f16_kernel(const float*
       vl[i >> 3][i & 7] = c;
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < EPT / 8; ++u) {
       *reinterpret_cast<half8*>(&kls[0][skey * kEaLd + sd + 8 * u]) = kh[u];
       *reinterpret_cast<half8*>(&vls[0][skey * kEaLd + sd + 8 * u]) = vh[u];
       if constexpr (NS == 2) {
@@ -366,10 +368,22 @@ hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Floa
     else
       hipLaunchKernelGGL((encoder_attention_kernel<1>), grid, block, 0, st, qkv, T, H, tiled);
   } else {
-    if (ns == 2)
-      hipLaunchKernelGGL((encoder_attention_f16_kernel<2>), grid, block, 0, st, qkv, T, H, tiled);
-    else
-      hipLaunchKernelGGL((encoder_attention_f16_kernel<1>), grid, block, 0, st, qkv, T, H, tiled);
+    static const int nw = [] {  // WA_ENC_ATTN_WAVES = 4 or 8 (32 queries per wave)
+      const char* e = getenv("WA_ENC_ATTN_WAVES");
+      return e && atoi(e) == 4 ? 4 : 8;
+    }();
+    const dim3 g2((T + 32 * nw - 1) / (32 * nw), H, B);
+    if (nw == 8) {
+      if (ns == 2)
+        hipLaunchKernelGGL((encoder_attention_f16_kernel<2, 8>), g2, dim3(512), 0, st, qkv, T, H, tiled);
+      else
+        hipLaunchKernelGGL((encoder_attention_f16_kernel<1, 8>), g2, dim3(512), 0, st, qkv, T, H, tiled);
+    } else {
+      if (ns == 2)
+        hipLaunchKernelGGL((encoder_attention_f16_kernel<2, 4>), g2, dim3(256), 0, st, qkv, T, H, tiled);
+      else
+        hipLaunchKernelGGL((encoder_attention_f16_kernel<1, 4>), g2, dim3(256), 0, st, qkv, T, H, tiled);
+    }
   }
   return hipGetLastError();
 }
