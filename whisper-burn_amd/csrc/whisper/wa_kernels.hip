@@ -421,9 +421,8 @@ __device__ __forceinline__ void attn_scan(const floatx4 (&qv)[TQ], int Tq, int k
 #pragma unroll
       for (int t = 0; t < TQ; ++t) {
         if (t < Tq) {
-          float dot = qv[t][0] * kk[u][0] + qv[t][1] * kk[u][1] + qv[t][2] * kk[u][2] + qv[t][3] * kk[u][3];
-#pragma unroll
-          for (int off = 1; off < 16; off <<= 1) dot += __shfl_xor(dot, off, 64);
+          const float dot =
+              wq4::sum16(qv[t][0] * kk[u][0] + qv[t][1] * kk[u][1] + qv[t][2] * kk[u][2] + qv[t][3] * kk[u][3]);
           if (j < k1 && vis(t, j)) {
             const float mn = fmaxf(m[t], dot);
             const float alpha = __builtin_amdgcn_exp2f(m[t] - mn);  // base-2 units

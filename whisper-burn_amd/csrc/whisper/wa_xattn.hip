@@ -174,8 +174,8 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   constexpr int HR = HT == 2 ? 1 : HT;  // score head tiles held in registers
   static_assert(CW * NW == D && CW % 32 == 0 && HT <= 2 && (PF == 1 || PF == 2), "bad column split");
   __shared__ __attribute__((aligned(16))) _Float16 se[kTc * RS];
-  __shared__ float red[NW][HT][16][17];
-  __shared__ __attribute__((aligned(16))) _Float16 sp[NS][32][kTc];
+  __shared__ __attribute__((aligned(16))) float red[NW][HT][16][20];  // row stride 20: conflict-free b128 stores
+  __shared__ __attribute__((aligned(16))) _Float16 sp[NS][32][kTc + 8];  // row stride 12 dwords: conflict-free P reads
   __shared__ float salpha[32];
   __shared__ int srescale[2];
   __shared__ __attribute__((aligned(16))) _Float16 sq1[HT == 2 ? NS : 1][4][HT == 2 ? D + 16 : 8];
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     }
   }
   // rows of P past the score tiles stay 0, their alpha 1
-  for (int i = tid; i < NS * 32 * kTc; i += kThreads) (&sp[0][0][0])[i] = (_Float16)0.0f;
+  for (int i = tid; i < NS * 32 * (kTc + 8); i += kThreads) (&sp[0][0][0])[i] = (_Float16)0.0f;
   if (tid < 32) salpha[tid] = 1.0f;
   if (tid < 2) srescale[tid] = 0;
 
@@ -248,6 +248,13 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   // tile; lane 4q+pp addresses row q, columns 4pp..4pp+3
   const int g = l >> 4, gi = l & 15;
   const int trow = 8 * (g >> 1) + (gi >> 2), tcol = 16 * (g & 1) + 4 * (gi & 3);
+  // se swizzle: row t keeps its 16-B slots at slot ^ sw(t), sw(t) = 3 for
+  // t >= 8 (a permutation inside each aligned 4-slot block).  With the row
+  // stride == 4 slots (mod 16) it spreads the score reads' 16-lane
+  // ds_read_b128 groups over all 16 slots of the bank row (2-way conflicts
+  // without it) and leaves the transposed reads' 32-lane groups conflict-free.
+  const int tcol_sw = ((((tcol >> 3) ^ ((g >> 1) ? 3 : 0)) << 3) | (tcol & 7));
+  const int lq_sw = lq ^ ((l16 & 8) ? 3 : 0);
 
   float sink = 0.0f;
   // scores of this wave's column slice: A = enc (m = frame, k = column) from
@@ -281,11 +288,8 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
       }
     }
 #pragma unroll
-    for (int ht = 0; ht < HT; ++ht)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) red[w][ht][l16][4 * lq + j] = sacc[ht][j];
+    for (int ht = 0; ht < HT; ++ht) *reinterpret_cast<floatx4*>(&red[w][ht][l16][4 * lq]) = sacc[ht];
     __syncthreads();
-
   };
   // online softmax of the sub-chunk's scores (red) and the Z update from se
   auto tail = [&](int chi, int t0) {
@@ -301,18 +305,14 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
         for (int ww = 0; ww < NW; ++ww) sv += red[ww][ht][hh][t];
         const bool valid = h < H && t0 + t < te;
         sv = valid ? sv : -INFINITY;
-        float cm = sv;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
+        const float cm = wq4::max16(sv);  // DPP butterfly over the head's 16 frames
         const float mn = fmaxf(M[e], cm);
         float alpha = 1.0f, p = 0.0f;
         if (mn != -INFINITY) {
           alpha = __builtin_amdgcn_exp2f(M[e] - mn);
           p = valid ? __builtin_amdgcn_exp2f(sv - mn) : 0.0f;
         }
-        float ps = p;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) ps += __shfl_xor(ps, o, 64);
+        const float ps = wq4::sum16(p);
         L[e] = L[e] * alpha + ps;
         M[e] = mn;
         _Float16 phi, plo;
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
       half8 eb[NS];
 #pragma unroll
       for (int p = 0; p < NS; ++p) {
-        const _Float16* base = &se[trow * RS + p * D + c0 + ct * 32 + tcol];
+        const _Float16* base = &se[trow * RS + p * D + c0 + ct * 32 + tcol_sw];
         const half4 x0 = lds_tr4(base);
         const half4 x1 = lds_tr4(base + 4 * RS);
         eb[p] = half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     for (int i = 0; i < NLD; ++i) {
       const int v = tid + i * kThreads;
       const int row = v / (ROW / 8), col = v - row * (ROW / 8);
-      if (v < NV) *reinterpret_cast<u32x4v*>(&se[row * RS + col * 8]) = buf[i];
+      if (v < NV) *reinterpret_cast<u32x4v*>(&se[row * RS + (col ^ ((row & 8) ? 3 : 0)) * 8]) = buf[i];
     }
     __syncthreads();
     if (MODE != 2 && chi + PF < nch) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
       return;
     }
     scores([&](int ks, int p) {
-      return *reinterpret_cast<const half8*>(&se[l16 * RS + p * D + c0 + ks * 32 + 8 * lq]);
+      return *reinterpret_cast<const half8*>(&se[l16 * RS + p * D + c0 + ks * 32 + 8 * lq_sw]);
     });
     tail(chi, t0);
   };

@@ -98,6 +98,35 @@ __device__ __forceinline__ int xcd_remap(int L, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// DPP lane read inside a row of 16 lanes -- a VALU operand modifier, no LDS
+// round trip as with ds_bpermute (__shfl_xor).  CTRL: 0xB1 quad_perm
+// [1,0,3,2] (lane ^ 1), 0x4E quad_perm [2,3,0,1] (lane ^ 2), 0x141
+// row_half_mirror (lane 7 - i of its 8), 0x140 row_mirror (lane 15 - i).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+
+// Butterfly sum / max over each aligned 16-lane group, result in every lane.
+// Bit-identical to the __shfl_xor butterfly over offsets 1, 2, 4, 8: after
+// the lane^1 and lane^2 steps a quad holds one value, so the half-mirror
+// partner (another quad of the 8) carries exactly what lane^4 would; after
+// that an 8-lane group holds one value and the mirror stands in for lane^8.
+__device__ __forceinline__ float sum16(float v) {
+  v += dpp_f32<0xB1>(v);
+  v += dpp_f32<0x4E>(v);
+  v += dpp_f32<0x141>(v);
+  v += dpp_f32<0x140>(v);
+  return v;
+}
+__device__ __forceinline__ float max16(float v) {
+  v = fmaxf(v, dpp_f32<0xB1>(v));
+  v = fmaxf(v, dpp_f32<0x4E>(v));
+  v = fmaxf(v, dpp_f32<0x141>(v));
+  v = fmaxf(v, dpp_f32<0x140>(v));
+  return v;
+}
+
 // Async 16-B-per-lane global -> LDS copy (global_load_lds_dwordx4): lane l's
 // 16 bytes land at lds_base + 16 * l (lds_base wave-uniform).
 __device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
