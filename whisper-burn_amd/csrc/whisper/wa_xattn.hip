@@ -178,6 +178,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   __shared__ __attribute__((aligned(16))) _Float16 sp[NS][32][kTc + 8];  // row stride 12 dwords: conflict-free P reads
   __shared__ float salpha[32];
   __shared__ int srescale[2];
+  __shared__ __attribute__((aligned(16))) _Float16 szero[8];
   __shared__ __attribute__((aligned(16))) _Float16 sq1[HT == 2 ? NS : 1][4][HT == 2 ? D + 16 : 8];
 
   const int s = blockIdx.x, r = blockIdx.y;
@@ -212,6 +213,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   for (int i = tid; i < NS * 32 * (kTc + 8); i += kThreads) (&sp[0][0][0])[i] = (_Float16)0.0f;
   if (tid < 32) salpha[tid] = 1.0f;
   if (tid < 2) srescale[tid] = 0;
+  if (tid < 8) szero[tid] = (_Float16)0.0f;
 
   floatx16 zacc[KS];
 #pragma unroll
@@ -227,19 +229,28 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     L[e] = 0.0f;
   }
 
-  // this range's frames through a buffer resource: rows past te (and the
-  // tail vectors when NV % threads != 0) read as zeros, no branches.  PF
-  // sub-chunks are in flight in registers while one is computed from LDS.
+  // this range's frames through a buffer resource: rows past te read as
+  // zeros, no branches.  Wave w fetches only its own column slice (16 frames
+  // x CW columns x NS planes): lane item v = plane-major, then frame, then
+  // 16-B piece, so one load instruction covers runs of CW * 2 contiguous
+  // bytes.  PF sub-chunks are in flight in registers while one is computed.
   typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  constexpr int PPR = CW / 8;  // 16-B pieces per frame row of the slice (one plane)
+  static_assert(NLD * 64 == NS * kTc * PPR, "the slice is a whole number of loads per lane");
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<_Float16*>(E + (size_t)ts * ROW), 0, nch > 0 ? (te - ts) * ROW * 2 : 0, 0x00020000);
+  auto item = [&](int i, int& row, int& col) {  // col: halves within the row (plane included)
+    const int v = l + 64 * i;
+    const int p = v / (kTc * PPR), rem = v - p * (kTc * PPR);
+    row = rem / PPR;
+    col = p * D + c0 + (rem - row * PPR) * 8;
+  };
   auto fetch = [&](u32x4v (&buf)[NLD], int chi) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
-      const int v = tid + i * kThreads;
-      const int row = v / (ROW / 8), col = v - row * (ROW / 8);
-      const uint32_t off = v < NV ? (uint32_t)((chi * kTc + row) * ROW * 2 + col * 16) : 0x7fffff00u;
-      buf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUX);
+      int row, col;
+      item(i, row, col);
+      buf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(((chi * kTc + row) * ROW + col) * 2), 0, AUX);
     }
   };
 
@@ -248,13 +259,24 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   // tile; lane 4q+pp addresses row q, columns 4pp..4pp+3
   const int g = l >> 4, gi = l & 15;
   const int trow = 8 * (g >> 1) + (gi >> 2), tcol = 16 * (g & 1) + 4 * (gi & 3);
-  // se swizzle: row t keeps its 16-B slots at slot ^ sw(t), sw(t) = 3 for
-  // t >= 8 (a permutation inside each aligned 4-slot block).  With the row
-  // stride == 4 slots (mod 16) it spreads the score reads' 16-lane
-  // ds_read_b128 groups over all 16 slots of the bank row (2-way conflicts
-  // without it) and leaves the transposed reads' 32-lane groups conflict-free.
-  const int tcol_sw = ((((tcol >> 3) ^ ((g >> 1) ? 3 : 0)) << 3) | (tcol & 7));
-  const int lq_sw = lq ^ ((l16 & 8) ? 3 : 0);
+  // se swizzle: frame row t keeps its 16-B slots at slot ^ sw(t), sw(t) = 3
+  // for t >= 8 (a permutation inside each aligned 4-slot block; slices start
+  // on 4-slot boundaries).  With the row stride == 4 slots (mod 16) it spreads
+  // the score reads' 16-lane ds_read_b128 groups over all 16 slots of the
+  // bank row and leaves the transposed reads' 32-lane groups and the 8-lane
+  // store groups conflict-free.  Every wave touches only its own slice, so
+  // the stores need no barrier before this wave's reads.
+  auto sw = [](int t) { return (t & 8) ? 3 : 0; };
+  const int tcol_sw = ((((tcol >> 3) ^ sw(trow)) << 3) | (tcol & 7));  // rows trow and trow + 4 share sw
+  const int lq_sw = lq ^ sw(l16);
+  auto write_se = [&](const u32x4v (&buf)[NLD]) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      int row, col;
+      item(i, row, col);
+      *reinterpret_cast<u32x4v*>(&se[row * RS + (((col >> 3) ^ sw(row)) << 3)]) = buf[i];
+    }
+  };
 
   float sink = 0.0f;
   // scores of this wave's column slice: A = enc (m = frame, k = column) from
@@ -275,9 +297,8 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
         for (int p = 0; p < NS; ++p) {
           if (ht < HR) {
             b[p] = qb[ht < HR ? ht : 0][ks][p];
-          } else {
-            b[p] = half8{0, 0, 0, 0, 0, 0, 0, 0};
-            if (l16 < 4) b[p] = *reinterpret_cast<const half8*>(&sq1[p][l16 & 3][c0 + ks * 32 + 8 * lq]);
+          } else {  // heads 16..19; the padding lanes read a zero fragment (no exec branch)
+            b[p] = *reinterpret_cast<const half8*>(l16 < 4 ? &sq1[p][l16 & 3][c0 + ks * 32 + 8 * lq] : szero);
           }
         }
         sacc[ht] = mfma16x32(a[0], b[0], sacc[ht]);
@@ -289,7 +310,6 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     }
 #pragma unroll
     for (int ht = 0; ht < HT; ++ht) *reinterpret_cast<floatx4*>(&red[w][ht][l16][4 * lq]) = sacc[ht];
-    __syncthreads();
   };
   // online softmax of the sub-chunk's scores (red) and the Z update from se
   auto tail = [&](int chi, int t0) {
@@ -327,7 +347,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     // alpha == 1 for every head (no running maximum moved, the steady state)
     // makes the rescale a multiplication by 1: skipped, bit-identical
     const bool rescale = srescale[chi & 1] != 0;
-    if (tid == 0) srescale[(chi + 1) & 1] = 0;  // next sub-chunk's flag; its writers come after two barriers
+    if (tid == 0) srescale[(chi + 1) & 1] = 0;  // next sub-chunk's flag; its writers come after the next score barrier
 
     // Z update: A = P (m = head, k = frame), B = enc (k = frame, n = column)
     half8 pa[NS];
@@ -358,16 +378,11 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
       }
     }
   };
+  // One sub-chunk: this wave's slice to se, the next fetch, the scores from
+  // se, then one barrier for the score partials and one inside tail().
   auto step = [&](u32x4v (&buf)[NLD], int chi) {
     const int t0 = ts + chi * kTc;
-    __syncthreads();  // previous sub-chunk's readers are done with se / sp
-#pragma unroll
-    for (int i = 0; i < NLD; ++i) {
-      const int v = tid + i * kThreads;
-      const int row = v / (ROW / 8), col = v - row * (ROW / 8);
-      if (v < NV) *reinterpret_cast<u32x4v*>(&se[row * RS + (col ^ ((row & 8) ? 3 : 0)) * 8]) = buf[i];
-    }
-    __syncthreads();
+    write_se(buf);
     if (MODE != 2 && chi + PF < nch) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
     if constexpr (MODE == 1) {  // probe: the load / LDS-write skeleton alone (one LDS read keeps it live)
       sink += (float)se[(tid * 9) % (kTc * RS)];
@@ -376,11 +391,13 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     scores([&](int ks, int p) {
       return *reinterpret_cast<const half8*>(&se[l16 * RS + p * D + c0 + ks * 32 + 8 * lq_sw]);
     });
+    __syncthreads();  // every wave's score partials in red
     tail(chi, t0);
   };
   u32x4v pre0[NLD];
   u32x4v pre1[PF == 2 ? NLD : 1];
   if (nch > 0) fetch(pre0, 0);
+  __syncthreads();  // sq1, sp, salpha, srescale, szero initialised
   if constexpr (PF == 2) {
     if (nch > 1) fetch(pre1, 1);
     for (int chi = 0; chi < nch; chi += 2) {
