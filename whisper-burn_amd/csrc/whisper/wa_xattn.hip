@@ -36,6 +36,7 @@ namespace {
 using wq4::atile_store4;
 using wq4::kbp_of;
 using wq4::split_f16;
+using wq4::half2v;
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
@@ -43,6 +44,7 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 constexpr int kWtQ4 = 0, kWtF16 = 1;  // raw weight formats (wa_model wtype)
 constexpr int kTc = 16;          // keys (encoder frames) per sub-chunk
 constexpr int kMaxD = 1280;
+constexpr float kXqScale = 0.125f * 1.4426950408889634f;  // 1 / sqrt(64) * log2(e)
 constexpr int kMaxSplits = 16;  // frame ranges per query row (merge weights in xattn_out_kernel LDS)
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -140,12 +142,83 @@ __global__ __launch_bounds__(256) void xattn_q_kernel(const float* __restrict__ 
       _Float16 x, y;
       // / sqrt(64) (attention.rs:262) * log2(e): scores in base-2 units, so
       // the softmax uses v_exp_f32 (2^x) directly
-      split_f16(acc[i] * (0.125f * 1.4426950408889634f), x, y);
+      split_f16(acc[i] * kXqScale, x, y);
       hi[i] = x;
       lo[i] = y;
     }
     *reinterpret_cast<half8*>(qt + (((size_t)r * NS + 0) * HP + h) * D + c0 + cc) = hi;
     if (NS == 2) *reinterpret_cast<half8*>(qt + (((size_t)r * NS + 1) * HP + h) * D + c0 + cc) = lo;
+  }
+}
+
+// MFMA form of xattn_q_kernel, same grid, 128 threads: out[r][c] = sum_d
+// q[r][h*64+d] Wk[h*64+d][c] as a 32 x 64 x 64 f16x2 product (A = q rows
+// split hi + lo from f32, B = the exact Wk values split hi + lo; the dropped
+// lo * lo term is < 2^-22 relative).  The 64 x 64 Wk block is dequantised
+// once into LDS transposed ([c][d], row stride 72 halves: conflict-free
+// fragment reads); wave w computes columns c0 + 32 w .. + 31.
+template <int NS, int WK>
+__global__ __launch_bounds__(128) void xattn_q_mfma_kernel(const float* __restrict__ q, int R, int D,
+                                                           const uint8_t* __restrict__ wk, int HP,
+                                                           _Float16* __restrict__ qt) {
+  constexpr int LD = 72;
+  __shared__ __attribute__((aligned(16))) _Float16 wth[64 * LD];
+  __shared__ __attribute__((aligned(16))) _Float16 wtl[64 * LD];
+  const int h = blockIdx.x, c0 = blockIdx.y * 64, r0 = blockIdx.z * 32, tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, l32 = l & 31, kh = l >> 5;
+  // A fragments: row l32, d = 16 ks + 8 kh .. + 7 (rows >= R read as zeros)
+  const int row = r0 + l32;
+  floatx4 xa[4][2];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      xa[ks][u] = row < R ? *reinterpret_cast<const floatx4*>(q + (size_t)row * D + h * 64 + ks * 16 + 8 * kh + 4 * u)
+                          : floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+  {  // thread (row d, block b) of the 64 x 2 Q4 blocks: exact values, split, stored transposed
+    const int d = tid >> 1, b = tid & 1;
+    float v[32];
+    load_w32<WK>(wk, D, h * 64 + d, (c0 >> 5) + b, v);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      _Float16 hi, lo;
+      split_f16(v[i], hi, lo);
+      wth[(b * 32 + i) * LD + d] = hi;
+      wtl[(b * 32 + i) * LD + d] = lo;
+    }
+  }
+  half8 ah[4], al[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      _Float16 x, y;
+      split_f16(xa[ks][j >> 2][j & 3], x, y);
+      ah[ks][j] = x;
+      al[ks][j] = y;
+    }
+  __syncthreads();
+  floatx16 acc = {};
+  const int c = 32 * w + l32;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const half8 bh = *reinterpret_cast<const half8*>(&wth[c * LD + ks * 16 + 8 * kh]);
+    const half8 bl = *reinterpret_cast<const half8*>(&wtl[c * LD + ks * 16 + 8 * kh]);
+    acc = mfma32x16(ah[ks], bh, acc);
+    acc = mfma32x16(al[ks], bh, acc);
+    acc = mfma32x16(ah[ks], bl, acc);
+  }
+  // acc[i]: row (i & 3) + 8 (i >> 2) + 4 kh, column c.  / sqrt(64)
+  // (attention.rs:262) * log2(e): scores in base-2 units for v_exp_f32
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int r = r0 + (i & 3) + 8 * (i >> 2) + 4 * kh;
+    if (r < R) {
+      _Float16 x, y;
+      split_f16(acc[i] * kXqScale, x, y);
+      qt[(((size_t)r * NS + 0) * HP + h) * D + c0 + c] = x;
+      if (NS == 2) qt[(((size_t)r * NS + 1) * HP + h) * D + c0 + c] = y;
+    }
   }
 }
 
@@ -162,7 +235,7 @@ template <int D, int HT, int NS, int NW, int PF, int AUX = 0, int MODE = 0>
 __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __restrict__ qt,
                                                              const _Float16* __restrict__ enc, int Tq, int T,
                                                              int H, int S, int CH, float* __restrict__ zpart,
-                                                             float* __restrict__ mlpart) {
+                                                             float* __restrict__ mlpart, int R, int xmap) {
   constexpr int kThreads = 64 * NW;
   constexpr int CW = D / NW;      // columns per wave
   constexpr int KS = CW / 32;     // 32-column steps per wave (score k-steps = Z column tiles)
@@ -181,7 +254,19 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   __shared__ __attribute__((aligned(16))) _Float16 szero[8];
   __shared__ __attribute__((aligned(16))) _Float16 sq1[HT == 2 ? NS : 1][4][HT == 2 ? D + 16 : 8];
 
-  const int s = blockIdx.x, r = blockIdx.y;
+  // xmap: 1-D grid of 8 * ceil(R / 8) * S workgroups dispatched round-robin
+  // over the 8 XCDs (L % 8); XCD x takes rows x, x + 8, ... with all their
+  // splits, so xattn_out (same map) reads the split partials from its own L2
+  int s, r;
+  if (xmap) {
+    const int L = blockIdx.x, x = L & 7, k = L >> 3;
+    s = k % S;
+    r = x + 8 * (k / S);
+    if (r >= R) return;  // whole workgroup, before any barrier
+  } else {
+    s = blockIdx.x;
+    r = blockIdx.y;
+  }
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int l16 = l & 15, lq = l >> 4, l32 = l & 31, lh = l >> 5;
   const _Float16* E = enc + (size_t)(r / Tq) * T * ROW;
@@ -434,22 +519,45 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
 
 // ---------------------------------------- merge + out = Wv Zn + bv --
 // grid (H, ceil(R / RPW)), 512 threads: the head's 64 raw Wv rows (46 KB of
-// Q4_0 blocks, LDS-DMA) and RPW rows of Zn ([column][row]) in LDS; thread
-// (row pair d, d + 32; blocks b, b + 16, b + 32) dequantizes each block once
-// for the RPW rows; 16 block-group partials per output are added through LDS
-// and out[r][h*64 + d] + bv goes into the A-tiled operand of the output
-// projection.  Fewer rows per workgroup spread the split-partial stream
-// (S * 5 KB per row and head) over more CUs.
-template <int NS, int WK, int RPW>
+// Q4_0 blocks, LDS-DMA) and RPW rows of Zn in LDS.  Q4 weights: the
+// projection runs on 16x16x32 MFMA (f16x2, waves split the K blocks, 8
+// partials per output); f16 weights: thread (row pair d, d + 32; blocks b,
+// b + 16, b + 32) on VALU, 16 partials.  The partials are added through LDS
+// in a fixed order and out[r][h*64 + d] + bv goes into the A-tiled operand of
+// the output projection.  Fewer rows per workgroup spread the split-partial
+// stream (S * 5 KB per row and head) over more CUs.
+template <int NS, int WK, int RPW, int SM>
 __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict__ zpart,
                                                         const float* __restrict__ mlpart, int R, int H, int D, int S,
                                                         const uint8_t* __restrict__ wv,
-                                                        const float* __restrict__ bv, _Float16* __restrict__ tiled) {
+                                                        const float* __restrict__ bv, _Float16* __restrict__ tiled,
+                                                        int xmap) {
   constexpr int kStage = WK == kWtQ4 ? 64 * (kMaxD / 32) * 18 : 16;  // 46 KB of Q4 blocks
   __shared__ __attribute__((aligned(16))) uint8_t sw[kStage];
-  __shared__ __attribute__((aligned(16))) float zs[kMaxD * RPW];  // [column][row]
+  // Zn of the RPW rows: f32 [column][row] (f16 weights, VALU projection) or
+  // f16 hi / lo planes [row][column] (Q4 weights, MFMA projection)
+  constexpr int ZLD = kMaxD + 8;  // halves; == 4 dwords (mod 64): conflict-free B fragment reads
+  __shared__ __attribute__((aligned(16))) uint8_t zbuf[WK == kWtQ4 ? 2 * RPW * ZLD * 2 : kMaxD * RPW * 4];
+  float* zs = reinterpret_cast<float*>(zbuf);
+  _Float16* zh = reinterpret_cast<_Float16*>(zbuf);
+  _Float16* zl = zh + RPW * ZLD;
+  __shared__ __attribute__((aligned(16))) _Float16 zzero[8];
   __shared__ float red[16][64][RPW + 1];
-  const int h = blockIdx.x, r0 = blockIdx.y * RPW, tid = threadIdx.x;
+  // rows rbase + rstep * j; xmap (see xattn_main_kernel): 1-D grid, XCD x =
+  // L % 8 takes rows x + 8 (RPW g + j) of head h
+  int h, rbase, rstep;
+  if (xmap) {
+    const int L = blockIdx.x, x = L & 7, k = L >> 3;
+    h = k % H;
+    rbase = x + 8 * RPW * (k / H);
+    rstep = 8;
+    if (rbase >= R) return;  // no rows here (R < 8): whole workgroup, before any barrier
+  } else {
+    h = blockIdx.x;
+    rbase = blockIdx.y * RPW;
+    rstep = 1;
+  }
+  const int tid = threadIdx.x;
   const int nkb = D / 32;
   // the value bias of this thread's final outputs, loaded up front
   const float bias1 = tid < 64 * RPW ? bv[h * 64 + (tid & 63)] : 0.0f;
@@ -465,79 +573,130 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
   }
   // merge of the S frame ranges (flash-attention merge, fixed split order):
   // Zn[c] = (sum_s w_s Z_s[c]) / (sum_s w_s L_s), w_s = exp(M_s - max_s M_s).
-  // Item (row j, 4 columns): the row's (M_s, L_s) and every split's float4
-  // are loaded together (fixed unrolled count; splits >= S read nothing), so
-  // the merge costs one memory round trip; rows >= R give zeros.
+  // Item (row j, 4 columns): the row's (M_s, L_s) and every split's float4.
+  // All NIT items of a thread are loaded before any is merged (fixed
+  // unrolled counts; splits >= S read nothing), so the merge costs one memory
+  // round trip; rows >= R give zeros.
   {
     const int nq = D / 4;
-    for (int it = tid; it < RPW * nq; it += 512) {
-      const int j = it / nq, q = it - j * nq;
-      const bool rok = r0 + j < R;
-      const size_t rb = (size_t)(rok ? r0 + j : 0) * S;
-      const floatx4* zp = reinterpret_cast<const floatx4*>(zpart + (rb * H + h) * D) + q;
-      const floatx2* mp = reinterpret_cast<const floatx2*>(mlpart) + rb * H + h;
-      floatx4 zv[kMaxSplits];
-      floatx2 ml[kMaxSplits];
+    constexpr int NIT = (RPW * (kMaxD / 4) + 511) / 512;
+    floatx4 zv[NIT][SM];
+    floatx2 ml[NIT][SM];
 #pragma unroll
-      for (int s = 0; s < kMaxSplits; ++s)
+    for (int u = 0; u < NIT; ++u) {
+      const int it = tid + 512 * u;
+      const int j = it / nq, q = it - j * nq;
+      const bool ok = it < RPW * nq && rbase + rstep * j < R;
+      const size_t rb = (size_t)(ok ? rbase + rstep * j : 0) * S;
+      const floatx4* zp = reinterpret_cast<const floatx4*>(zpart + (rb * H + h) * D) + (ok ? q : 0);
+      const floatx2* mp = reinterpret_cast<const floatx2*>(mlpart) + rb * H + h;
+#pragma unroll
+      for (int s = 0; s < SM; ++s)
         if (s < S) {
-          ml[s] = mp[(size_t)s * H];
-          zv[s] = zp[(size_t)s * H * (D / 4)];
+          ml[u][s] = mp[(size_t)s * H];
+          zv[u][s] = zp[(size_t)s * H * (D / 4)];
         }
+    }
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+      const int it = tid + 512 * u;
+      if (it >= RPW * nq) break;
+      const int j = it / nq, q = it - j * nq;
+      const bool rok = rbase + rstep * j < R;
       float mx = -INFINITY;
 #pragma unroll
-      for (int s = 0; s < kMaxSplits; ++s)
-        if (s < S) mx = fmaxf(mx, ml[s][0]);
+      for (int s = 0; s < SM; ++s)
+        if (s < S) mx = fmaxf(mx, ml[u][s][0]);
       float lsum = 0.0f;
       floatx4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int s = 0; s < kMaxSplits; ++s)
+      for (int s = 0; s < SM; ++s)
         if (s < S) {
-          const float w = ml[s][0] == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(ml[s][0] - mx);  // base-2 units
-          lsum = fmaf(w, ml[s][1], lsum);
+          const float w = ml[u][s][0] == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(ml[u][s][0] - mx);  // base-2 units
+          lsum = fmaf(w, ml[u][s][1], lsum);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[e] = fmaf(w, zv[s][e], acc[e]);
+          for (int e = 0; e < 4; ++e) acc[e] = fmaf(w, zv[u][s][e], acc[e]);
         }
+      if constexpr (WK == kWtQ4) {
+        half4 hi, lo;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) zs[(4 * q + e) * RPW + j] = rok ? acc[e] / lsum : 0.0f;
+        for (int e = 0; e < 4; ++e) {
+          _Float16 x, y;
+          split_f16(rok ? acc[e] / lsum : 0.0f, x, y);
+          hi[e] = x;
+          lo[e] = y;
+        }
+        *reinterpret_cast<half4*>(&zh[j * ZLD + 4 * q]) = hi;
+        *reinterpret_cast<half4*>(&zl[j * ZLD + 4 * q]) = lo;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) zs[(4 * q + e) * RPW + j] = rok ? acc[e] / lsum : 0.0f;
+      }
     }
   }
+  if (tid < 8) zzero[tid] = (_Float16)0.0f;
   if (WK == kWtQ4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stage pieces landed
   __syncthreads();
-  const int dp = tid & 31, bg = tid >> 5;  // rows dp, dp + 32; blocks bg, bg + 16, bg + 32
-  float acc0[RPW], acc1[RPW];
+  constexpr int NPART = WK == kWtQ4 ? 8 : 16;  // partials per output in red
+  if constexpr (WK == kWtQ4) {
+    // out^T (d x row) = Wv_h (64 x D) Zn^T on 16x16x32 MFMA: m = 16 outputs d
+    // (4 tiles), n = the rows (RPW real of 16), k = one Q4 block of 32
+    // columns.  Wave w takes blocks w, w + 8, ...; A = the exact weights
+    // (q - 8) d split hi + lo, B = Zn hi / lo: three products as elsewhere.
+    // Lane l: A row d = 16 mt + (l & 15), elements 8 (l >> 4) .. + 7 of the
+    // block = low (l >> 4 < 2) or high nibbles of nibble bytes 8 ((l >> 4) & 1)
+    // .. + 7; B row n = l & 15, the same 8 columns.
+    const int w = tid >> 6, l = tid & 63, n = l & 15, lq = l >> 4;
+    const int sh = (lq >> 1) * 4;
+    floatx4 acc[4];
 #pragma unroll
-  for (int j = 0; j < RPW; ++j) {
-    acc0[j] = 0.0f;
-    acc1[j] = 0.0f;
-  }
-#pragma unroll 1
-  for (int kb = bg; kb < nkb; kb += 16) {
-    if (WK == kWtQ4) {
-      // word i of the 16 nibble bytes holds elements 2i, 2i+1 (low nibbles)
-      // and 16+2i, 17+2i (high nibbles) of the block
-      const uint16_t* b0 = reinterpret_cast<const uint16_t*>(&sw[(size_t)dp * rowbytes + (size_t)kb * 18]);
-      const uint16_t* b1 = reinterpret_cast<const uint16_t*>(&sw[(size_t)(dp + 32) * rowbytes + (size_t)kb * 18]);
-      const float d0 = (float)__builtin_bit_cast(_Float16, b0[0]);
-      const float d1 = (float)__builtin_bit_cast(_Float16, b1[0]);
-#pragma unroll 2
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t t0 = b0[1 + i], t1 = b1[1 + i];
-        const int e[4] = {2 * i, 2 * i + 1, 16 + 2 * i, 17 + 2 * i};
-        const int sh[4] = {0, 8, 4, 12};
+    for (int mt = 0; mt < 4; ++mt) acc[mt] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int kb = w; kb < nkb; kb += 8) {
+      const _Float16* zhp = n < RPW ? &zh[n * ZLD + kb * 32 + 8 * lq] : zzero;
+      const _Float16* zlp = n < RPW ? &zl[n * ZLD + kb * 32 + 8 * lq] : zzero;
+      const half8 bh = *reinterpret_cast<const half8*>(zhp);
+      const half8 bl = *reinterpret_cast<const half8*>(zlp);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float wa = (float)((int)((t0 >> sh[q]) & 15u) - 8) * d0;
-          const float wb = (float)((int)((t1 >> sh[q]) & 15u) - 8) * d1;
-          const float* z = &zs[(kb * 32 + e[q]) * RPW];
+      for (int mt = 0; mt < 4; ++mt) {
+        const uint16_t* blk = reinterpret_cast<const uint16_t*>(&sw[(size_t)(mt * 16 + n) * rowbytes + (size_t)kb * 18]);
+        const _Float16 d = __builtin_bit_cast(_Float16, blk[0]);
+        const half2v off = {(_Float16)1032.0f, (_Float16)1032.0f};
+        const half2v dv = {d, d};
+        half8 ah, al;
 #pragma unroll
-          for (int j = 0; j < RPW; ++j) {
-            acc0[j] = fmaf(wa, z[j], acc0[j]);
-            acc1[j] = fmaf(wb, z[j], acc1[j]);
-          }
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t x = (uint32_t)blk[1 + 4 * (lq & 1) + i] >> sh;
+          const uint32_t pr = (x & 0xFu) | ((x << 8) & 0xF0000u) | 0x64006400u;
+          const half2v qv = __builtin_bit_cast(half2v, pr) - off;  // exact q - 8
+          const half2v hv = qv * dv;
+          const half2v lv = __builtin_elementwise_fma(qv, dv, -hv);  // exact remainder
+          ah[2 * i] = hv[0];
+          ah[2 * i + 1] = hv[1];
+          al[2 * i] = lv[0];
+          al[2 * i + 1] = lv[1];
         }
+        acc[mt] = mfma16x32(ah, bh, acc[mt]);
+        acc[mt] = mfma16x32(ah, bl, acc[mt]);
+        acc[mt] = mfma16x32(al, bh, acc[mt]);
       }
-    } else {
+    }
+    // acc[mt][i]: output d = 16 mt + 4 lq + i, row n
+    if (n < RPW) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[w][16 * mt + 4 * lq + i][n] = acc[mt][i];
+    }
+  } else {
+    const int dp = tid & 31, bg = tid >> 5;  // rows dp, dp + 32; blocks bg, bg + 16, bg + 32
+    float acc0[RPW], acc1[RPW];
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      acc0[j] = 0.0f;
+      acc1[j] = 0.0f;
+    }
+#pragma unroll 1
+    for (int kb = bg; kb < nkb; kb += 16) {
       float w0[32], w1[32];
       load_w32<WK>(wv, D, h * 64 + dp, kb, w0);
       load_w32<WK>(wv, D, h * 64 + dp + 32, kb, w1);
@@ -551,18 +710,18 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
         }
       }
     }
-  }
 #pragma unroll
-  for (int j = 0; j < RPW; ++j) {
-    red[bg][dp][j] = acc0[j];
-    red[bg][dp + 32][j] = acc1[j];
+    for (int j = 0; j < RPW; ++j) {
+      red[bg][dp][j] = acc0[j];
+      red[bg][dp + 32][j] = acc1[j];
+    }
   }
   __syncthreads();
   if (tid < 64 * RPW) {  // thread (row j, output d): the block-group sum in group order, then 4-wide stores
-    const int j = tid >> 6, d = tid & 63, r = r0 + j;
+    const int j = tid >> 6, d = tid & 63, r = rbase + rstep * j;
     float sacc = bias1;
 #pragma unroll
-    for (int g = 0; g < 16; ++g) sacc += red[g][d][j];
+    for (int g = 0; g < NPART; ++g) sacc += red[g][d][j];
     const float v1 = __shfl_down(sacc, 1, 64), v2 = __shfl_down(sacc, 2, 64), v3 = __shfl_down(sacc, 3, 64);
     if (r < R && (d & 3) == 0) atile_store4<NS>(tiled, r, h * 64 + d, kbp_of(D), sacc, v1, v2, v3);
   }
@@ -601,7 +760,7 @@ __global__ __launch_bounds__(256) void untile_kernel(const _Float16* __restrict_
 // fit the register file at Large-V3 f16x2.
 template <int D, int HT, int NS>
 void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T, int H, int S, int CH, float* z,
-                 float* ml, hipStream_t st) {
+                 float* ml, int R, int xmap, hipStream_t st) {
   static const int variant = [] {  // probe knob: 1 = the load skeleton alone (wrong results)
     const char* e = getenv("WA_XATTN_MAIN");
     return e ? atoi(e) : 0;
@@ -609,17 +768,19 @@ void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T,
   if constexpr ((D / 8) % 32 == 0) {
     if (variant == 2) {  // probe (wrong results): compute on the first sub-chunk only, no further loads
       hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1, 0, 2>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z,
-                         ml);
+                         ml, R, xmap);
       return;
     }
     if (variant == 1) {  // probe (wrong results): loads + LDS writes + barriers only
       hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1, 0, 1>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z,
-                         ml);
+                         ml, R, xmap);
       return;
     }
-    hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z, ml);
+    hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z, ml, R,
+                       xmap);
   } else {
-    hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 4, 1>), g, dim3(256), 0, st, qt, enc, Tq, T, H, S, CH, z, ml);
+    hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 4, 1>), g, dim3(256), 0, st, qt, enc, Tq, T, H, S, CH, z, ml, R,
+                       xmap);
   }
 }
 
@@ -634,13 +795,22 @@ int xattn_out_rows() {
 }
 template <int NS, int WK>
 void launch_out(int rpw, dim3 go, const float* z, const float* ml, int R, int H, int D, int S, const uint8_t* wv,
-                const float* bv, _Float16* tiled, hipStream_t st) {
-  if (rpw == 4)
-    hipLaunchKernelGGL((xattn_out_kernel<NS, WK, 4>), go, dim3(512), 0, st, z, ml, R, H, D, S, wv, bv, tiled);
-  else if (rpw == 2)
-    hipLaunchKernelGGL((xattn_out_kernel<NS, WK, 2>), go, dim3(512), 0, st, z, ml, R, H, D, S, wv, bv, tiled);
-  else
-    hipLaunchKernelGGL((xattn_out_kernel<NS, WK, 1>), go, dim3(512), 0, st, z, ml, R, H, D, S, wv, bv, tiled);
+                const float* bv, _Float16* tiled, int xmap, hipStream_t st) {
+  // SM: unrolled split slots of the merge (8 for the default plan)
+#define WA_XOUT(RPW_, SM_)                                                                                   \
+  hipLaunchKernelGGL((xattn_out_kernel<NS, WK, RPW_, SM_>),                                                  \
+                     xmap ? dim3(8 * H * ((R + 8 * (RPW_)-1) / (8 * (RPW_)))) : go, dim3(512), 0, st, z, ml, R, H, D, \
+                     S, wv, bv, tiled, xmap)
+  if (S > 8) {
+    WA_XOUT(4, kMaxSplits);  // larger split counts (WA_XATTN_SPLITS): 4 rows per workgroup
+  } else if (rpw == 4) {
+    WA_XOUT(4, 8);
+  } else if (rpw == 2) {
+    WA_XOUT(2, 8);
+  } else {
+    WA_XOUT(1, 8);
+  }
+#undef WA_XOUT
 }
 
 }  // namespace
@@ -695,7 +865,19 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   float* ml = part + (size_t)R * p.splits * H * D;
   // qt = Wk^T q / 8
   const dim3 gq(H, D / 64, (R + 31) / 32);
-  if (wtype == kWtQ4) {
+  static const bool q_mfma = [] {
+    const char* e = getenv("WA_XATTN_Q_MFMA");
+    return e ? atoi(e) != 0 : true;
+  }();
+  if (q_mfma) {
+#define WA_XQ(NS_, WK_) hipLaunchKernelGGL((xattn_q_mfma_kernel<NS_, WK_>), gq, dim3(128), 0, st, q, R, D, wk, HP, qt)
+    if (wtype == kWtQ4) {
+      if (ns == 2) WA_XQ(2, kWtQ4); else WA_XQ(1, kWtQ4);
+    } else {
+      if (ns == 2) WA_XQ(2, kWtF16); else WA_XQ(1, kWtF16);
+    }
+#undef WA_XQ
+  } else if (wtype == kWtQ4) {
     if (ns == 2)
       hipLaunchKernelGGL((xattn_q_kernel<2, kWtQ4>), gq, dim3(256), 0, st, q, R, D, wk, HP, qt);
     else
@@ -707,13 +889,20 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
       hipLaunchKernelGGL((xattn_q_kernel<1, kWtF16>), gq, dim3(256), 0, st, q, R, D, wk, HP, qt);
   }
   // stream the encoder output
-  const dim3 gm(p.splits, R);
+  // XCD-affine rows for xattn_main / xattn_out (WA_XATTN_XCD=1).  Off by
+  // default: measured 5 % slower per decode step with two 16-clip groups
+  // (the partials do not stay in the XCD's L2 across the kernel boundary).
+  static const int xmap = [] {
+    const char* e = getenv("WA_XATTN_XCD");
+    return e ? atoi(e) != 0 : 0;
+  }();
+  const dim3 gm = xmap ? dim3(8 * ((R + 7) / 8) * p.splits) : dim3(p.splits, R);
 #define WA_XMAIN(DD, HH)                                                          \
   if (D == DD && HT == HH) {                                                      \
     if (ns == 2)                                                                  \
-      launch_main<DD, HH, 2>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, st);   \
+      launch_main<DD, HH, 2>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, R, xmap, st);   \
     else                                                                          \
-      launch_main<DD, HH, 1>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, st);   \
+      launch_main<DD, HH, 1>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, R, xmap, st);   \
   } else
   WA_XMAIN(1280, 2)
   WA_XMAIN(1024, 1)
@@ -727,14 +916,14 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   const dim3 go(H, (R + rpw - 1) / rpw);
   if (wtype == kWtQ4) {
     if (ns == 2)
-      launch_out<2, kWtQ4>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
+      launch_out<2, kWtQ4>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, xmap, st);
     else
-      launch_out<1, kWtQ4>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
+      launch_out<1, kWtQ4>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, xmap, st);
   } else {
     if (ns == 2)
-      launch_out<2, kWtF16>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
+      launch_out<2, kWtF16>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, xmap, st);
     else
-      launch_out<1, kWtF16>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
+      launch_out<1, kWtF16>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, xmap, st);
   }
   return hipGetLastError();
 }

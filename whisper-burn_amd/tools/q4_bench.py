@@ -40,9 +40,14 @@ def rand_q4(n: int, k: int, seed: int) -> np.ndarray:
 
 
 def bench_shape(torch, m: int, n: int, k: int, prec: int, policy: int, iters: int, warmup: int = 3,
-                graph: bool = True) -> dict:
+                graph: bool = True, cold: int = 0) -> dict:
+    """cold > 0: the graph cycles through `cold` distinct weight tensors (more
+    bytes than the caches hold), so every launch reads its weights from HBM,
+    as the decoder's layer-by-layer chain does."""
     L = wq4.lib()
     t = wq4.Q4Tensor.from_q4_bytes(rand_q4(n, k, n * 31 + k), [n, k])
+    ts = [t] + [wq4.Q4Tensor.from_q4_bytes(rand_q4(n, k, n * 31 + k + i), [n, k]) for i in range(1, cold)]
+    it = [0]
     x = torch.randn((m, k), device="cuda:0", dtype=torch.float32)
     atb = L.wq4_atiled_bytes(m, k, prec)
     at = torch.empty(atb, dtype=torch.uint8, device="cuda:0")
@@ -56,7 +61,9 @@ def bench_shape(torch, m: int, n: int, k: int, prec: int, policy: int, iters: in
         wq4.set_kernel_policy(policy)
 
         def run():
-            wq4.check(L.wq4_linear_forward_tiled(t.handle, None, ctypes.c_void_p(at.data_ptr()), None,
+            w = ts[it[0] % len(ts)]
+            it[0] += 1
+            wq4.check(L.wq4_linear_forward_tiled(w.handle, None, ctypes.c_void_p(at.data_ptr()), None,
                                                  ctypes.c_void_p(y.data_ptr()), m, 0, prec, st))
 
         for _ in range(warmup):
@@ -98,6 +105,7 @@ def main() -> None:
     ap.add_argument("--decode-only", action="store_true")
     ap.add_argument("--shape", default=None, help="m,n,k: one prefill-kernel shape only (profiling)")
     ap.add_argument("--prec", type=int, default=0, help="with --shape: 0 f16x2, 1 f16")
+    ap.add_argument("--cold", type=int, default=0, help="decode shapes: cycle through N weight tensors")
     args = ap.parse_args()
     import torch
 
@@ -112,8 +120,9 @@ def main() -> None:
         for (n, k) in [(1280, 1280), (3840, 1280), (5120, 1280), (1280, 5120)]:
             for m in ([] if args.decode_only else enc_m):
                 rows.append(bench_shape(torch, m, n, k, prec, 1, args.iters, graph=not args.no_graph))
-            for m in (1, 32, 64):
-                rows.append(bench_shape(torch, m, n, k, prec, 2, args.iters, graph=not args.no_graph))
+            for m in (1, 16, 32, 64):
+                rows.append(bench_shape(torch, m, n, k, prec, 2, args.iters, graph=not args.no_graph,
+                                        cold=args.cold))
     for r in rows:
         print(f"{r['kernel']:8s} {r['prec']:6s} M={r['m']:6d} N={r['n']:5d} K={r['k']:5d}  {r['us']:9.1f} us  "
               f"{r['tflops']:7.1f} TF/s ({100 * r['frac_mfma']:5.1f}% MFMA)  {r['gbs']:7.0f} GB/s "
