@@ -1196,11 +1196,11 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_kernel(const float* __r
   pick_from_lds(lg, B, V, pval, pidx, counter, out_tok, &ticket);
 }
 
-// 16x16x32 form of logits_argmax_f16_kernel: a lane's embedding fragment
-// is 8 dims of one of 16 rows, so one load instruction covers 16 rows x 64
-// contiguous bytes (the 32x32x16 form: 32 rows x 32 B) -- half the rows
-// touched per instruction for the same bytes.  Wave = 32 vocabulary rows as
-// two 16-row m-tiles, the 32 clips as two n-tiles.
+// 16x16x32 form of logits_argmax_f16_kernel over the fragment-tiled table
+// (launch_emb_tiled): a lane's embedding fragment is 8 dims of one of 16
+// rows, stored so that one load instruction reads 1 KiB contiguous (the row-
+// major table gave 16 rows x 64 B per instruction).  Wave = 32 vocabulary
+// rows as two 16-row m-tiles, the 32 clips as two n-tiles.
 template <int NS>
 __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
     const float* __restrict__ hid, int B, int D, long ldh, const _Float16* __restrict__ emb2, int V, int min_tokens,
@@ -1212,12 +1212,10 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, lq = lane >> 4;
   const int v0 = blockIdx.x * 128 + wave * 32;
+  // fragment-tiled table (launch_emb_tiled): this wave's two 16-row groups
   const _Float16* er[2];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const int v = v0 + 16 * mt + l16;
-    er[mt] = emb2 + (size_t)(v < V ? v : V - 1) * NS * D;
-  }
+  for (int mt = 0; mt < 2; ++mt) er[mt] = emb2 + (size_t)(v0 / 16 + mt) * (D / 32) * NS * 512 + lane * 8;
   const int nch = (D + kLg2Chunk - 1) / kLg2Chunk;
   constexpr int KS = kLg2Chunk / 32;
   floatx4 acc[2][2];
@@ -1232,10 +1230,8 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-        for (int p = 0; p < NS; ++p) {
-          const int k = kc + 32 * ks + 8 * lq;
-          e[mt][ks][p] = *reinterpret_cast<const half8*>(er[mt] + (size_t)p * D + (k < D ? k : 0));
-        }
+        for (int p = 0; p < NS; ++p)  // D % kLg2Chunk == 0 (launcher): always in range
+          e[mt][ks][p] = *reinterpret_cast<const half8*>(er[mt] + ((size_t)(kc / 32 + ks) * NS + p) * 512);
   };
   // the hidden rows of a chunk (f32, thread: row e / 32, 4 dims) travel one
   // chunk ahead in registers too, so no chunk waits on a dependent load
@@ -1329,19 +1325,58 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
 
 int logits_argmax_groups(int V) { return (V + 127) / 128; }
 
+// f32 rows -> fragment-tiled f16 planes; thread = (group, step, lane): 8 values
+template <int NS>
+__global__ __launch_bounds__(256) void emb_tiled_kernel(const float* __restrict__ x, int V, int D, int64_t nfrag,
+                                                        _Float16* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nfrag * 64) return;
+  const int lane = (int)(i & 63);
+  const int64_t f = i >> 6;  // g * (D / 32) + s
+  const int64_t g = f / (D / 32);
+  const int s = (int)(f - g * (D / 32));
+  const int64_t v = g * 16 + (lane & 15);
+  const int k = s * 32 + 8 * (lane >> 4);
+  half8 hi, lo;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    _Float16 a = (_Float16)0.0f, b = (_Float16)0.0f;
+    if (v < V) split_f16(x[v * D + k + j], a, b);
+    hi[j] = a;
+    lo[j] = b;
+  }
+  *reinterpret_cast<half8*>(out + (f * NS + 0) * 512 + lane * 8) = hi;
+  if constexpr (NS == 2) *reinterpret_cast<half8*>(out + (f * NS + 1) * 512 + lane * 8) = lo;
+}
+
+bool emb_tiled_supported(int D) { return D % kLg2Chunk == 0; }
+int64_t emb_tiled_rows(int V) { return (int64_t)logits_argmax_groups(V) * 128; }
+
+hipError_t launch_emb_tiled(const float* emb, int V, int D, int ns, _Float16* out, hipStream_t st) {
+  if (!emb_tiled_supported(D) || (ns != 1 && ns != 2)) return hipErrorInvalidValue;
+  const int64_t nfrag = emb_tiled_rows(V) / 16 * (D / 32);
+  const dim3 g((unsigned)((nfrag * 64 + 255) / 256));
+  if (ns == 2)
+    hipLaunchKernelGGL(emb_tiled_kernel<2>, g, dim3(256), 0, st, emb, V, D, nfrag, out);
+  else
+    hipLaunchKernelGGL(emb_tiled_kernel<1>, g, dim3(256), 0, st, emb, V, D, nfrag, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const float* emb, const _Float16* emb2,
-                                int ns, int V, int min_tokens, const DecodeState* state, float* pval, int* pidx,
-                                int* counter, int* out_tok, hipStream_t st) {
+                                int emb2_tiled, int ns, int V, int min_tokens, const DecodeState* state, float* pval,
+                                int* pidx, int* counter, int* out_tok, hipStream_t st) {
   if (B < 1 || B > 32 || D % 16 != 0 || !state) return hipErrorInvalidValue;
   const dim3 grid(logits_argmax_groups(V));
-  static const bool k32 = [] {  // WA_LOGITS_K32=0: the 32x32x16 form (A/B)
-    const char* e = getenv("WA_LOGITS_K32");
-    return e ? atoi(e) != 0 : true;
-  }();
-  if (emb2 && ns == 2 && k32 && D % kLg2Chunk == 0)
-    hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<2>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens,
-                       state, pval, pidx, counter, out_tok);
-  else if (emb2 && ns == 2)
+  if (emb2 && emb2_tiled) {
+    if (!emb_tiled_supported(D)) return hipErrorInvalidValue;
+    if (ns == 2)
+      hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<2>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens,
+                         state, pval, pidx, counter, out_tok);
+    else
+      hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<1>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens,
+                         state, pval, pidx, counter, out_tok);
+  } else if (emb2 && ns == 2)
     hipLaunchKernelGGL(logits_argmax_f16_kernel<2>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens, state,
                        pval, pidx, counter, out_tok);
   else if (emb2)

@@ -87,11 +87,22 @@ hipError_t launch_argmax(const float* logits, int B, int V, int lo, int hi, int 
 // D % 8 == 0; pval / pidx: 32 * logits_argmax_groups(V) scratch each,
 // counter: one int zeroed once (re-armed by the kernel).
 int logits_argmax_groups(int V);
-// emb2 != nullptr: the f16-pair table [V][ns][D] (launch_enc_planes of emb)
-// on f16 MFMA; else the f32 table on f32 MFMA.  D % 16 == 0.
+// emb2 != nullptr: the f16-pair table on f16 MFMA -- fragment-tiled
+// (launch_emb_tiled) when emb2_tiled, else [V][ns][D] (launch_enc_planes of
+// emb); else the f32 table on f32 MFMA.  D % 16 == 0.
 hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const float* emb, const _Float16* emb2,
-                                int ns, int V, int min_tokens, const DecodeState* state, float* pval, int* pidx,
-                                int* counter, int* out_tok, hipStream_t st);
+                                int emb2_tiled, int ns, int V, int min_tokens, const DecodeState* state, float* pval,
+                                int* pidx, int* counter, int* out_tok, hipStream_t st);
+// Whether the logits kernel reads a fragment-tiled table for this width.
+bool emb_tiled_supported(int D);
+// Rows of the fragment-tiled table (V padded to the kernel's 128-row groups).
+int64_t emb_tiled_rows(int V);
+// f32 [V][D] -> fragment-tiled f16 planes: per 16-row group g, 32-column
+// step s and plane p, the 16x16x32 MFMA operand of 64 lanes x 8 halves is
+// 1 KiB contiguous at ((g * D / 32 + s) * ns + p) KiB (lane = 16 (k / 8 % 4)
+// + row % 16), rows >= V zero -- every load instruction of the logits
+// kernel reads 1 KiB contiguous.  out: emb_tiled_rows(V) * ns * D halves.
+hipError_t launch_emb_tiled(const float* emb, int V, int D, int ns, _Float16* out, hipStream_t st);
 
 // Greedy-loop bookkeeping at the top of each step (whisper.rs:104-115):
 // for every clip not yet done, EOT -> done (eot_stop != 0), else append the

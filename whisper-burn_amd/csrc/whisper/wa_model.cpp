@@ -197,7 +197,8 @@ struct wa_model {
   // globals
   float *conv1_wt, *conv1_b, *conv2_wt, *conv2_b, *enc_pos, *lnp_w, *lnp_b;
   float *tok_emb, *dec_pos, *dln_w, *dln_b;
-  _Float16* tok_emb2 = nullptr;  // tied embedding as f16 pairs [V][ns][D] for the step's logits
+  _Float16* tok_emb2 = nullptr;  // tied embedding as f16 pairs for the step's logits
+  int emb2_tiled = 0;            // tok_emb2 fragment-tiled (wa::launch_emb_tiled), else [V][ns][D]
   std::vector<EncLayer> enc;
   std::vector<DecLayer> dec;
   // encoder activations
@@ -603,11 +604,17 @@ wq4_status alloc_activations(wa_model* m) {
     L.cache_k = f32((int64_t)B * c.n_text_ctx * Dt);
     L.cache_v = f32((int64_t)B * c.n_text_ctx * Dt);
   }
-  // f16-pair tied embedding for the decode step's fused logits + pick
-  m->tok_emb2 = d.alloc<_Float16>((size_t)c.n_vocab * m->ns * Dt);
+  // f16-pair tied embedding for the decode step's fused logits + pick,
+  // fragment-tiled (1 KiB contiguous per load instruction) where supported
+  m->emb2_tiled = wa::emb_tiled_supported(Dt) ? 1 : 0;
+  const size_t erows = m->emb2_tiled ? (size_t)wa::emb_tiled_rows(c.n_vocab) : (size_t)c.n_vocab;
+  m->tok_emb2 = d.alloc<_Float16>(erows * m->ns * Dt);
   if (!m->tok_emb2) return fail(WQ4_ENOMEM, "embedding plane allocation failed");
-  m->bytes += (size_t)c.n_vocab * m->ns * Dt * 2;
-  WA_HIP(wa::launch_enc_planes(m->tok_emb, c.n_vocab, Dt, m->ns, m->tok_emb2, nullptr));
+  m->bytes += erows * m->ns * Dt * 2;
+  if (m->emb2_tiled)
+    WA_HIP(wa::launch_emb_tiled(m->tok_emb, c.n_vocab, Dt, m->ns, m->tok_emb2, nullptr));
+  else
+    WA_HIP(wa::launch_enc_planes(m->tok_emb, c.n_vocab, Dt, m->ns, m->tok_emb2, nullptr));
   // cross-attention scratch, sized for the largest plan over 1..4B rows
   const int HP = (c.n_text_head + 15) / 16 * 16;
   size_t xpart = 0;
@@ -849,8 +856,8 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
   // position of every clip (decoder.rs:289-292, 342-343)
   WA_WQ4(wq4_layernorm(g.xd, m->dln_w, m->dln_b, rows, D, WQ4_PREC_F16X2, nullptr, g.hid, st));
   if (fused_pick(g, Tq, state)) {  // decode step: logits + greedy pick in one kernel, into next_tok
-    WA_HIP(wa::launch_logits_argmax(g.hid, B, D, D, m->tok_emb, m->tok_emb2, m->ns, c.n_vocab, kMinTokens, state,
-                                    g.lg_val, g.lg_idx, g.lg_ctr, g.next_tok, st));
+    WA_HIP(wa::launch_logits_argmax(g.hid, B, D, D, m->tok_emb, m->tok_emb2, m->emb2_tiled, m->ns, c.n_vocab,
+                                    kMinTokens, state, g.lg_val, g.lg_idx, g.lg_ctr, g.next_tok, st));
     return WQ4_OK;
   }
   WA_HIP(wa::launch_logits(g.hid + (size_t)(Tq - 1) * D, B, D, (int64_t)Tq * D, m->tok_emb, c.n_vocab, g.logits,
