@@ -170,3 +170,20 @@ def test_f16_gguf_checkpoint(torch, tmp_path):
     assert g.weights == "f16"
     mel = torch.from_numpy(mels(2, first=9)).cuda()
     assert torch.equal(g.encode(mel), s.encode(mel))
+
+
+def test_two_decode_groups_match_oracle(torch, oracle_model, gpu_model):
+    """16 clips take the two-stream decode path (two groups of 8, each its own
+    graph and KV cache, wa_model.cpp decode_groups); their tokens must equal
+    the single-group path's (batches of 4) and the oracle's for a sample."""
+    import whisper_amd
+
+    m16 = whisper_amd.WhisperModel("tiny_test", SEED, max_batch=16)
+    mel = mels(16, first=20)
+    got = m16.transcribe(torch.from_numpy(mel).cuda(), 50259, max_tokens=24)
+    assert len(got) == 16
+    for c0 in range(0, 16, 4):
+        assert gpu_model.transcribe(torch.from_numpy(mel[c0:c0 + 4]).cuda(), 50259, max_tokens=24) == got[c0:c0 + 4]
+    sample = [0, 7, 8, 15]  # first and last clip of each group
+    assert oracle_model.transcribe(mel[sample], 50259, max_tokens=24) == [got[i] for i in sample]
+    m16.close()
