@@ -187,3 +187,29 @@ def test_two_decode_groups_match_oracle(torch, oracle_model, gpu_model):
     sample = [0, 7, 8, 15]  # first and last clip of each group
     assert oracle_model.transcribe(mel[sample], 50259, max_tokens=24) == [got[i] for i in sample]
     m16.close()
+
+
+@pytest.mark.parametrize("eot_scale", [10.0, 12.0])
+def test_ragged_eot_stop_matches_oracle(torch, tmp_path, eot_scale):
+    """Ragged end of transcript (whisper.rs:104-125): the EOT row of the token
+    embedding is scaled so that some clips emit EOT after the 3 forced tokens
+    and others run to max_tokens (oracle lengths at 10x: one clip of six stops
+    at 7 tokens; at 12x most stop at 3). Finished clips keep running masked in
+    their decode group, a group whose clips are all done stops replaying, and
+    every clip's tokens must equal the oracle's, through both decode groups."""
+    import whisper_amd
+    import write_gguf
+
+    tensors = write_gguf.synthetic_tensors("tiny_test", SEED)
+    tensors["decoder.token_embedding.weight"][wo.EOT] *= eot_scale
+    p = tmp_path / "eot.gguf"
+    write_gguf.write_gguf(str(p), tensors, "eot")
+    g = whisper_amd.WhisperModel.from_gguf(str(p), "tiny_test", max_batch=16)
+    ref = wo.SynthWhisper("tiny_test", SEED)
+    ref.w["decoder.token_embedding.weight"][wo.EOT] *= eot_scale
+    mel = mels(16, first=30)
+    want = ref.transcribe(mel, 50259, max_tokens=24)
+    assert len({len(t) for t in want}) > 1  # the case is ragged
+    got = g.transcribe(torch.from_numpy(mel).cuda(), 50259, max_tokens=24)
+    assert got == want
+    g.close()
