@@ -213,3 +213,25 @@ def test_ragged_eot_stop_matches_oracle(torch, tmp_path, eot_scale):
     got = g.transcribe(torch.from_numpy(mel).cuda(), 50259, max_tokens=24)
     assert got == want
     g.close()
+
+
+# ------------------------------------- full-size models (BASELINE configs) --
+@pytest.mark.parametrize("variant,n_mels,batch", [("large_v3", 128, 32), ("medium", 80, 16)])
+def test_full_size_batch_invariance(torch, variant, n_mels, batch):
+    """At the bench's full sizes the numpy oracle is too slow, so parity rests
+    on a size-independent property: a clip's encoder output and tokens are the
+    same alone (B = 1: one decode group, M = 1 GEMV plans, 1500-row encoder
+    GEMMs) as inside a full batch (two decode groups, 48000-row encoder GEMMs
+    at Large-V3) -- bit for bit, since every kernel's per-row arithmetic is
+    batch-independent by construction."""
+    import whisper_amd
+
+    m = whisper_amd.WhisperModel(variant, SEED, max_batch=batch)
+    mel = torch.from_numpy(mels(batch, n_mels=n_mels, first=40)).cuda()
+    enc = m.encode(mel)
+    got = m.transcribe(mel, 50259, max_tokens=32)
+    assert len(got) == batch
+    for i in (0, batch // 2 - 1, batch // 2, batch - 1):  # first and last clip of each decode group
+        assert torch.equal(m.encode(mel[i:i + 1])[0], enc[i])
+        assert m.transcribe(mel[i:i + 1], 50259, max_tokens=32)[0] == got[i]
+    m.close()
