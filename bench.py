@@ -90,6 +90,24 @@ def pmc_traffic(kernel: str):
     return None if v is None else v.get("hbm_bytes_per_launch")
 
 
+def pmc_traffic_xattn_probe(rows: int, heads: int):
+    """HBM bytes of one decode-step cross-attention at the bench probe's shape
+    (all `rows` clips in one launch): xattn_q (grid independent of the rows)
+    + xattn_main (8 frame splits x 512 work-items per row) + xattn_out (512
+    work-items per head per 4 rows), from the grid-split PMC summary --
+    the same three kernels `achieved` is timed over.  None if not measured."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            k = json.load(f).get("kernels", {})
+        q = k["xattn_q_kernel"]["hbm_bytes_per_launch"]
+        main = k["xattn_main_kernel"]["by_grid_items"][str(8 * 512 * rows)]["hbm_bytes_per_launch"]
+        out = k["xattn_out_kernel"]["by_grid_items"][str(heads * 512 * ((rows + 3) // 4))]["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        return None
+    return q + main + out
+
+
 def cpu_baseline(cfg: dict, rows: int, tokens: float) -> dict:
     """Reference CPU dequant -> naive GEMM on one encoder layer's Q4 GEMMs."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -237,7 +255,8 @@ def main() -> None:
         xa = probe["cross_attention"]
         xa_gbs = xa["bytes"] / (xa["us"] * 1e-6) * 1e-9
         roof_xa = {"bound": "hbm", "achieved": round(xa_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                   "frac": round(xa_gbs / PEAK_HBM_GBS, 4), "traffic": pmc_traffic("xattn_main_kernel"),
+                   "frac": round(xa_gbs / PEAK_HBM_GBS, 4),
+                   "traffic": pmc_traffic_xattn_probe(B, cfg["n_text_head"]),
                    "kernel": "cross-attention over the encoder output: xattn_q + xattn_main + xattn_out "
                              "(split merge fused; decode step, Tq = 1)", "avg_us": round(xa["us"], 2),
                    "bytes_per_launch": xa["bytes"],

@@ -16,11 +16,22 @@ import sys
 
 FAMILIES = {"q4_gemm_prefill_kernel": r"q4_gemm_prefill_kernel", "q4_gemm_decode_kernel": r"q4_gemm_decode_kernel",
             "xattn_main_kernel": r"xattn_main_kernel",
-            "xattn_q_kernel": r"xattn_q_kernel", "xattn_merge_kernel": r"xattn_merge_kernel",
+            "xattn_q_kernel": r"xattn_q_\w*kernel", "xattn_merge_kernel": r"xattn_merge_kernel",
             "xattn_out_kernel": r"xattn_out_kernel"}
 
 
-def load(counter: str, rnd: str) -> dict:
+def grid_items(row: dict) -> int:
+    """Total work-items of the dispatch (Grid_Size, or the product of Grid_Size_X/Y/Z)."""
+    if row.get("Grid_Size"):
+        return int(float(row["Grid_Size"]))
+    n = 1
+    for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"):
+        if row.get(k):
+            n *= int(float(row[k]))
+    return n
+
+
+def load(counter: str, rnd: str, by_grid: dict | None = None) -> dict:
     files = glob.glob(f"gpurun_out/pmc_{counter}_{rnd}/**/*counter_collection*.csv", recursive=True)
     per = {}
     for fn in files:
@@ -31,12 +42,15 @@ def load(counter: str, rnd: str) -> dict:
             for fam, rx in FAMILIES.items():
                 if re.search(rx, name):
                     per.setdefault(fam, []).append(float(row["Counter_Value"]))
+                    if by_grid is not None:
+                        by_grid.setdefault((fam, grid_items(row)), []).append(float(row["Counter_Value"]))
     return per
 
 
 def main() -> None:
     rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
-    fetch, write = load("FETCH_SIZE", rnd), load("WRITE_SIZE", rnd)
+    gf, gw = {}, {}
+    fetch, write = load("FETCH_SIZE", rnd, gf), load("WRITE_SIZE", rnd, gw)
     out = {"round": rnd, "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; "
                                    "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch",
            "kernels": {}}
@@ -47,6 +61,16 @@ def main() -> None:
         fk, wk = sum(f) / len(f), sum(w) / len(w)
         out["kernels"][fam] = {"launches_fetch": len(f), "launches_write": len(w), "fetch_size_kib": fk,
                                "write_size_kib": wk, "hbm_bytes_per_launch": (2 * fk + wk) * 1024}
+        # the same family split by dispatch size (work-items): decode groups,
+        # prompts and the bench's all-clip probe launch differ only in grid
+        grids = {}
+        for (fam2, g), fv in sorted(gf.items()):
+            wv = gw.get((fam2, g), [])
+            if fam2 != fam or not wv:
+                continue
+            a, b = sum(fv) / len(fv), sum(wv) / len(wv)
+            grids[str(g)] = {"launches": len(fv), "hbm_bytes_per_launch": (2 * a + b) * 1024}
+        out["kernels"][fam]["by_grid_items"] = grids
     dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     with open(dst, "w") as fh:
