@@ -19,10 +19,15 @@ during the timed steps; algorithmic FLOPs = 2*M*N*K per launch) or the decode
 step's cross-attention (HBM stream of every clip's encoder output, f16 hi/lo
 planes, shared by all heads -- no per-layer K/V caches; HIP-event timed by
 wa_probe_kernels right after the timed steps; algorithmic bytes = encoder
-planes + raw Wk, Wv + operands).  Both, and the decode-step fc1 GEMM, are reported.  cpu_baseline: the reference's CPU dequant->GEMM
-path (src/gguf/tests.rs:60-87,172-184, restated in oracle/q4_oracle.c), one
-core, on one Large-V3 encoder layer's Q4 GEMMs at --cpu-rows rows, scaled to
-a clip's Q4 GEMM FLOPs (a lower bound on the CPU's per-clip time).
+planes + raw Wk, Wv + operands).  Both, and the decode-step fc1 GEMM, are reported.
+
+cpu_baseline: the reference's CPU dequant->GEMM path
+(src/gguf/tests.rs:60-87,172-184, restated in oracle/q4_oracle.c) on
+Q4Linear 1280x1280 and Q4FFN 1280->5120->1280 at M = 1, 32, 1500, run (i) on
+one core and run (ii) on every core of this process, CPU model printed; the
+clip's Q4 GEMM time is extrapolated from those x layer counts.  Emitted by
+rank 0 at every world size.  Multi-rank runs use a gloo (host) group for the
+barriers and the MAX of the timed seconds: RCCL is never initialised.
 """
 from __future__ import annotations
 
@@ -65,9 +70,20 @@ def max_over_ranks(x: float, dist, device) -> float:
         return x
     import torch
 
-    t = torch.tensor([x], device=device, dtype=torch.float64)
+    t = torch.tensor([x], device=device, dtype=torch.float64)  # device "cpu": gloo
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def init_dist():
+    """Process group of a multi-rank run: gloo over the host.  The only
+    cross-rank traffic is the barriers and one MAX of the timed-region seconds,
+    so RCCL is never initialised (no collective on the data
+    path).  Rendezvous from the torch.distributed.run environment."""
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    return dist
 
 
 def job_rtf(world: int, B: int, steps: int, elapsed: float) -> float:
@@ -75,63 +91,147 @@ def job_rtf(world: int, B: int, steps: int, elapsed: float) -> float:
     return world * B * steps * CLIP_SECONDS / elapsed
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+def _pmc_kernels(workload: dict):
+    """Kernel table of the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by scripts/pmc_summary.py from separate
     FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per MI355X_MICROARCH.md
-    'HBM'), or None when absent."""
+    'HBM'), or None when absent or when it profiled another workload (variant,
+    weights, precision, clips): a summary is never borrowed across runs."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    v = d.get("kernels", {}).get(kernel)
+    if d.get("workload") != workload:
+        return None
+    return d.get("kernels", {})
+
+
+def pmc_traffic(kernel: str, workload: dict):
+    """HBM bytes per launch of `kernel` (all its launches), or None."""
+    k = _pmc_kernels(workload)
+    v = None if k is None else k.get(kernel)
     return None if v is None else v.get("hbm_bytes_per_launch")
 
 
-def pmc_traffic_xattn_probe(rows: int, heads: int):
-    """HBM bytes of one decode-step cross-attention at the bench probe's shape
-    (all `rows` clips in one launch): xattn_q (grid independent of the rows)
-    + xattn_main (8 frame splits x 512 work-items per row) + xattn_out (512
-    work-items per head per 4 rows), from the grid-split PMC summary --
-    the same three kernels `achieved` is timed over.  None if not measured."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+def pmc_traffic_grid(kernel: str, grid_items: int, workload: dict):
+    """HBM bytes per launch of `kernel` at one dispatch size (total
+    work-items), or None."""
+    k = _pmc_kernels(workload)
     try:
-        with open(path) as f:
-            k = json.load(f).get("kernels", {})
-        q = k["xattn_q_kernel"]["hbm_bytes_per_launch"]
-        main = k["xattn_main_kernel"]["by_grid_items"][str(8 * 512 * rows)]["hbm_bytes_per_launch"]
-        out = k["xattn_out_kernel"]["by_grid_items"][str(heads * 512 * ((rows + 3) // 4))]["hbm_bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
+        return k[kernel]["by_grid_items"][str(grid_items)]["hbm_bytes_per_launch"]
+    except (TypeError, KeyError):
         return None
-    return q + main + out
 
 
-def cpu_baseline(cfg: dict, rows: int, tokens: float) -> dict:
-    """Reference CPU dequant -> naive GEMM on one encoder layer's Q4 GEMMs."""
+def pmc_traffic_xattn_probe(rows: int, heads: int, d_model: int, workload: dict):
+    """HBM bytes of one decode-step cross-attention at the bench probe's shape
+    (all `rows` clips in one launch), each kernel looked up at its own grid
+    (work-items): xattn_q (H x D/64 x ceil(rows/32) workgroups of 128),
+    xattn_main (8 frame splits x 512 work-items per row), xattn_out (512
+    work-items per head per 4 rows) -- the launches `achieved` is timed over.
+    None if not measured for this workload."""
+    parts = [pmc_traffic_grid("xattn_q_kernel", heads * (d_model // 64) * ((rows + 31) // 32) * 128, workload),
+             pmc_traffic_grid("xattn_main_kernel", 8 * 512 * rows, workload),
+             pmc_traffic_grid("xattn_out_kernel", heads * 512 * ((rows + 3) // 4), workload)]
+    return None if any(p is None for p in parts) else sum(parts)
+
+
+def cpu_threads() -> int:
+    """Host cores this process may use: the affinity mask, capped by
+    OMP_NUM_THREADS where the box sets it (the GPU box's CPU share)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+CPU_ROWS = (1, 32, 1500)
+
+
+def cpu_shape_times(D: int, nthreads: int, sample_rows: int) -> dict:
+    """Q4Linear D x D and Q4FFN D -> 4D -> D on the reference's
+    CPU path (dequantize + naive i-j-l matmul, tests.rs:60-87,172-184), at
+    M = 1, 32, 1500 rows.  The naive loop is linear in M, so M = 1500 is timed
+    on min(sample_rows, 1500) rows and scaled by 1500 / rows (the per-call
+    dequant, < 2 % of such a call, is scaled with it).  Returns {name: {"rows_timed", "s", "gflops"}}."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
 
     import oracle
 
-    D = cfg["n_audio_state"]
-    shapes = [(D, D)] * 4 + [(4 * D, D), (D, 4 * D)]  # q, k, v, out, fc1, fc2
     rng = np.random.default_rng(0)
-    t = 0.0
-    flops = 0.0
-    for n, k in shapes:
-        q = oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.02).astype(np.float32))
-        x = rng.standard_normal(rows * k).astype(np.float32)
-        t0 = time.perf_counter()
-        oracle.cpu_dequant_gemm(q, x, rows, k, n)
-        t += time.perf_counter() - t0
-        flops += 2.0 * rows * n * k
-    sec_per_clip = t * (clip_q4_gflop(cfg, tokens) * 1e9 / flops)
-    return {"value": CLIP_SECONDS / sec_per_clip, "unit": "audio-s/wall-s", "cores": 1, "kind": "port",
-            "sample": f"one Large-V3 encoder layer's 6 Q4 GEMMs at {rows} rows ({flops * 1e-9:.1f} GFLOP, "
-                      f"{t:.1f} s, {flops / t * 1e-9:.2f} GFLOP/s), scaled to {clip_q4_gflop(cfg, tokens):.0f} "
-                      f"GFLOP of Q4 GEMMs per clip (lower bound on CPU time)"}
+    F = 4 * D
+    w = {n: oracle.quantize_convert_np((rng.standard_normal(a * b) * 0.02).astype(np.float32))
+         for n, a, b in (("lin", D, D), ("fc1", F, D), ("fc2", D, F))}
+    b_d = (rng.standard_normal(D) * 0.01).astype(np.float32)
+    b_f = (rng.standard_normal(F) * 0.01).astype(np.float32)
+    out = {}
+    for m in CPU_ROWS:
+        r = min(m, sample_rows)
+        x = rng.standard_normal(r * D).astype(np.float32)
+        for name, flop_per_row in (("q4linear", 2.0 * D * D), ("q4ffn", 4.0 * D * F)):
+            t0 = time.perf_counter()
+            if name == "q4linear":
+                oracle.cpu_linear(w["lin"], b_d, x, r, D, D, nthreads)
+            else:
+                oracle.cpu_ffn(w["fc1"], b_f, w["fc2"], b_d, x, r, D, F, nthreads)
+            t = time.perf_counter() - t0
+            s = t * m / r
+            out[f"{name}_M{m}"] = {"rows_timed": r, "s": round(s, 5), "gflops": round(flop_per_row * m / s * 1e-9, 3)}
+    return out
+
+
+def cpu_clip_seconds(cfg: dict, shapes: dict, tokens: float) -> float:
+    """Extrapolated CPU seconds of one clip's Q4 GEMMs: encoder
+    and cross-K/V projections at M = 1500 rows, prompt + greedy decode at
+    M = 1 row per token (the reference decodes one clip at a time), from the
+    per-shape timings x layer counts.  The model's other ops are not counted:
+    a lower bound on the reference CPU path's clip time."""
+    lin = lambda m: shapes[f"q4linear_M{m}"]["s"]
+    ffn = lambda m: shapes[f"q4ffn_M{m}"]["s"]
+    enc = cfg["n_audio_layer"] * (4 * lin(1500) + ffn(1500))
+    cross = cfg["n_text_layer"] * 2 * lin(1500)
+    per_tok = cfg["n_text_layer"] * (6 * lin(1) + ffn(1))
+    return enc + cross + per_tok * (4 + tokens)
+
+
+def cpu_baseline(cfg: dict, rows: int, tokens: float) -> dict:
+    """The reference's CPU dequant -> GEMM path timed on this box:
+    run (i) one core, as the reference runs it; run (ii) all cores of this
+    process (OpenMP over outputs, this build's parallelisation).  value = run
+    (i)'s extrapolated real-time factor of one clip's Q4 GEMMs."""
+    D = cfg["n_audio_state"]
+    n_all = cpu_threads()
+    t0 = time.perf_counter()
+    single = cpu_shape_times(D, 1, rows)
+    multi = cpu_shape_times(D, n_all, 1500) if n_all > 1 else single
+    wall = time.perf_counter() - t0
+    c1 = cpu_clip_seconds(cfg, single, tokens)
+    cn = cpu_clip_seconds(cfg, multi, tokens)
+    return {"value": round(CLIP_SECONDS / c1, 4), "unit": "audio-s/wall-s", "cores": 1, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"Q4Linear {D}x{D} and Q4FFN {D}->{4 * D}->{D} at M = 1, 32, 1500 rows on the reference's CPU "
+                      f"path (dequantize + naive f32 matmul, tests.rs:60-87,172-184, oracle/q4_oracle.c); run (i) 1 "
+                      f"core (M = 1500 timed on {min(rows, 1500)} rows, scaled), run (ii) {n_all} cores (OpenMP over "
+                      f"outputs, all 1500 rows); value = 30 s / one clip's Q4 GEMM seconds extrapolated from the "
+                      f"shape timings x layer counts ({tokens:.0f} tokens, M = 1 decode); {wall:.1f} s of CPU timing",
+            "single_core": {"cores": 1, "clip_q4_s_extrapolated": round(c1, 2), "shapes": single},
+            "all_cores": {"cores": n_all, "value": round(CLIP_SECONDS / cn, 4),
+                          "clip_q4_s_extrapolated": round(cn, 2), "shapes": multi}}
 
 
 def main() -> None:
@@ -150,7 +250,8 @@ def main() -> None:
                     help="start from 16 kHz samples in HBM: the GPU log-mel front-end (wa_log_mel) runs inside "
                          "the timed region")
     ap.add_argument("--fixed-length", action="store_true", help="ignore EOT (always max-tokens steps)")
-    ap.add_argument("--cpu-rows", type=int, default=750)
+    ap.add_argument("--cpu-rows", type=int, default=160,
+                    help="rows the single-core CPU baseline times at M = 1500 (scaled to 1500)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--json-out", default=None)
@@ -166,11 +267,7 @@ def main() -> None:
     import wq4
 
     torch.cuda.set_device(local_rank)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    dist = init_dist() if world > 1 else None
     prec = wq4.PREC_F16X2 if args.precision == "f16x2" else wq4.PREC_F16
     t_load = time.perf_counter()
     model = whisper_amd.WhisperModel(args.variant, args.seed, max_batch=args.clips_per_gpu, device=local_rank,
@@ -234,21 +331,32 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     model.profile_enable(False)
     prof = model.profile_read(reset=True)
-    elapsed = max_over_ranks(elapsed, dist, f"cuda:{local_rank}")
+    # PCIe-inclusive figure (never `value`): one batch's inputs from pinned host
+    # memory to HBM, timed after the timed steps and added per step
+    host_in = inputs[0].cpu().pin_memory()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(3):
+        inputs[0].copy_(host_in, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d_s = (time.perf_counter() - t1) / 3
+    elapsed_pcie = max_over_ranks(elapsed + args.steps * h2d_s, dist, "cpu")
+    elapsed = max_over_ranks(elapsed, dist, "cpu")
     clips = world * B * args.steps
     value = job_rtf(world, B, args.steps, elapsed)
 
     probe = model.probe_kernels(B, iters=20) if rank == 0 else None
     if rank == 0:
+        workload = {"variant": args.variant, "weights": args.weights, "precision": args.precision, "clips": B}
         q4 = prof["q4_gemm"]
         mean_tok = float(np.mean(ntok)) if ntok else 0.0
         steps_run = float(np.mean([t["steps"] for t in timings])) if timings else 0.0
-        # north-star kernel: the Q4 MFMA tile GEMMs (encoder + cross-K/V), timed live per launch
+        # north-star kernel: the Q4 MFMA tile GEMMs of the encoder, timed live per launch
         q4_tf = q4["gflop"] / (q4["ms"] * 1e-3) * 1e-3 if q4["ms"] > 0 else 0.0
         roof_q4 = {"bound": "mfma", "achieved": round(q4_tf, 2), "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s",
                    "frac": round(q4_tf / PEAK_MFMA_TFLOPS, 4),
-                   "traffic": pmc_traffic("q4_gemm_prefill_kernel"),
-                   "kernel": "q4_gemm_prefill_kernel (encoder + cross-K/V Q4 GEMMs)",
+                   "traffic": pmc_traffic("q4_gemm_prefill_kernel", workload),
+                   "kernel": "q4_gemm_prefill_kernel (encoder Q4 GEMMs)",
                    "launches": q4["launches"], "avg_us": round(q4["ms"] / max(1, q4["launches"]) * 1e3, 2),
                    "total_ms_per_step": round(q4["ms"] / args.steps, 2)}
         # decode phase: cross-attention (HBM stream of the cached K/V), probed after the timed steps
@@ -256,7 +364,7 @@ def main() -> None:
         xa_gbs = xa["bytes"] / (xa["us"] * 1e-6) * 1e-9
         roof_xa = {"bound": "hbm", "achieved": round(xa_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                    "frac": round(xa_gbs / PEAK_HBM_GBS, 4),
-                   "traffic": pmc_traffic_xattn_probe(B, cfg["n_text_head"]),
+                   "traffic": pmc_traffic_xattn_probe(B, cfg["n_text_head"], cfg["n_text_state"], workload),
                    "kernel": "cross-attention over the encoder output: xattn_q + xattn_main + xattn_out "
                              "(split merge fused; decode step, Tq = 1)", "avg_us": round(xa["us"], 2),
                    "bytes_per_launch": xa["bytes"],
@@ -292,13 +400,12 @@ def main() -> None:
                          for k in ("encoder_ms", "cross_kv_ms", "prompt_ms", "decode_ms")},
             "decode_steps": [t["steps"] for t in timings],
             "input": "16 kHz audio in HBM (GPU log-mel timed)" if args.audio else "log-mel in HBM",
+            "input_h2d_ms_per_step": round(h2d_s * 1e3, 3),
+            "value_pcie_inclusive": round(job_rtf(world, B, args.steps, elapsed_pcie), 3),
             "log_mel_ms": round(float(np.mean(mel_ms)), 3) if mel_ms else None,
             "model_load_s": round(t_load, 2),
         }
-        if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(model.config, args.cpu_rows, mean_tok)
-        else:
-            line["cpu_baseline"] = None
+        line["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline(model.config, args.cpu_rows, mean_tok)
         s = json.dumps(line)
         print(s, flush=True)
         if args.json_out:

@@ -59,6 +59,8 @@ def lib() -> ctypes.CDLL:
         L.q4o_ffn.argtypes = [u8p, f32p, u8p, f32p, f32p, i64, i64, i64, i64, f32p, f32p]
         L.q4o_cpu_dequant_gemm.argtypes = [u8p, f32p, i64, i64, i64, f32p, f32p]
         L.q4o_closed_form.argtypes = [ctypes.c_int, i64, f32p]
+        L.q4o_cpu_linear.argtypes = [u8p, f32p, f32p, i64, i64, i64, f32p, f32p, ctypes.c_int]
+        L.q4o_cpu_ffn.argtypes = [u8p, f32p, u8p, f32p, f32p, i64, i64, i64, f32p, f32p, f32p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -162,6 +164,30 @@ def cpu_dequant_gemm(q4: np.ndarray, x: np.ndarray, M: int, K: int, N: int) -> n
     lib().q4o_cpu_dequant_gemm(_u8p(np.ascontiguousarray(q4, np.uint8)), _f32p(np.ascontiguousarray(x, np.float32)),
                                M, K, N, _f32p(deq), _f32p(out))
     return out.reshape(M, N)
+
+
+def cpu_linear(q4, bias, x, M: int, K: int, N: int, nthreads: int = 1) -> np.ndarray:
+    """SURVEY §8(d) CPU baseline: Q4Linear on the reference's CPU path
+    (dequantize tests.rs:60-87 + naive matmul :172-184 + bias linear.rs:37-39);
+    nthreads > 1 = OpenMP over the outputs (same bits)."""
+    deq = np.empty(N * K, np.float32)
+    out = np.empty(M * N, np.float32)
+    bp = None if bias is None else _f32p(np.ascontiguousarray(bias, np.float32))
+    lib().q4o_cpu_linear(_u8p(np.ascontiguousarray(q4, np.uint8)), bp, _f32p(np.ascontiguousarray(x, np.float32)),
+                         M, K, N, _f32p(deq), _f32p(out), int(nthreads))
+    return out.reshape(M, N)
+
+
+def cpu_ffn(fc1, b1, fc2, b2, x, M: int, D: int, F: int, nthreads: int = 1) -> np.ndarray:
+    """SURVEY §8(d) CPU baseline: Q4FFN (layers.rs:54-58) on the CPU path."""
+    deq = np.empty(F * D, np.float32)
+    h = np.empty(M * F, np.float32)
+    out = np.empty(M * D, np.float32)
+    lib().q4o_cpu_ffn(_u8p(np.ascontiguousarray(fc1, np.uint8)), _f32p(np.ascontiguousarray(b1, np.float32)),
+                      _u8p(np.ascontiguousarray(fc2, np.uint8)), _f32p(np.ascontiguousarray(b2, np.float32)),
+                      _f32p(np.ascontiguousarray(x, np.float32)), M, D, F, _f32p(deq), _f32p(h), _f32p(out),
+                      int(nthreads))
+    return out.reshape(M, D)
 
 
 # ------------------------------------------------------------ numpy oracle --

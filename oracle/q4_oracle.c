@@ -254,6 +254,50 @@ void q4o_cpu_dequant_gemm(const uint8_t* q4, const float* x, int64_t M, int64_t 
   q4o_reference_matmul(x, deq, M, K, N, out);
 }
 
+/* ---- the CPU baseline of SURVEY.md §8(d), run (i) and run (ii) -----------
+ * Q4Linear::forward on the CPU path the reference has: dequantize
+ * (tests.rs:60-87) + naive i-j-l f32 matmul (tests.rs:172-184) + bias
+ * (linear.rs:37-39); Q4FFN::forward = fc1 -> gelu -> fc2 (layers.rs:54-58).
+ * nthreads = 1 is the reference's single-threaded loop (run (i)); nthreads > 1
+ * is this build's OpenMP parallelisation (run (ii)): dequant blocks and the
+ * (row, column) outputs of the matmul are shared out statically, each output
+ * still summed in the reference's l order, so both runs give the same bits.
+ * deq: caller scratch [N*K]; the FFN's h: [M*F]. */
+static void cpu_dequant_mt(const uint8_t* q4, int64_t n, float* out, int nthreads) {
+  int64_t nb = n / Q4_BLOCK;
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+  for (int64_t b = 0; b < nb; ++b) q4o_dequantize(q4 + b * Q4_BYTES, Q4_BLOCK, out + b * Q4_BLOCK);
+}
+
+static void cpu_matmul_mt(const float* a, const float* bt, int64_t m, int64_t k, int64_t n, float* out,
+                          int nthreads) {
+#pragma omp parallel for collapse(2) schedule(static) num_threads(nthreads)
+  for (int64_t i = 0; i < m; ++i)
+    for (int64_t j = 0; j < n; ++j) {
+      float acc = 0.0f;
+      const float* ar = a + i * k;
+      const float* br = bt + j * k;
+      for (int64_t l = 0; l < k; ++l) acc += ar[l] * br[l];
+      out[i * n + j] = acc;
+    }
+}
+
+void q4o_cpu_linear(const uint8_t* q4, const float* bias, const float* x, int64_t M, int64_t K, int64_t N,
+                    float* deq, float* out, int nthreads) {
+  cpu_dequant_mt(q4, N * K, deq, nthreads);
+  cpu_matmul_mt(x, deq, M, K, N, out, nthreads);
+  if (bias)
+    for (int64_t r = 0; r < M; ++r)
+      for (int64_t c = 0; c < N; ++c) out[r * N + c] = out[r * N + c] + bias[c];
+}
+
+void q4o_cpu_ffn(const uint8_t* fc1, const float* b1, const uint8_t* fc2, const float* b2, const float* x,
+                 int64_t M, int64_t D, int64_t F, float* deq, float* h, float* out, int nthreads) {
+  q4o_cpu_linear(fc1, b1, x, M, D, F, deq, h, nthreads);
+  q4o_gelu(h, M * F);
+  q4o_cpu_linear(fc2, b2, h, M, F, D, deq, out, nthreads);
+}
+
 /* ---- closed-form inputs of the reference tests (Rust f32 sin/cos) -------
  * kind 0: ((i*0.001).sin()*0.1)          tests.rs:432-434, 493-495, 515-517
  * kind 1: ((i*0.0007).cos()*0.05)        tests.rs:436-438

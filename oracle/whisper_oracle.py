@@ -246,11 +246,20 @@ class SynthWhisper:
         return int(len(v) - 1 - np.argmax(v[::-1]))
 
     def transcribe(self, mel: np.ndarray, lang_token: int | None = 50259, max_tokens: int = MAX_TOKENS,
-                   eot_stop: bool = True, return_logits: bool = False):
-        """WhisperModel::transcribe (whisper.rs:51-128), batched over clips."""
+                   eot_stop: bool = True, return_logits: bool = False, trace: dict | None = None):
+        """WhisperModel::transcribe (whisper.rs:51-128), batched over clips.
+
+        trace (a dict, optional) receives "enc" (the encoder output) and
+        "picked" (the logit vectors [B, V] every greedy pick was taken from, EOT
+        already suppressed where whisper.rs:97-98,120-122 suppresses it: the
+        prompt's pick first, then one per decode step) -- the full-size
+        fixtures of tests/golden/make_full_size.py."""
         c = self.cfg
         B = mel.shape[0]
         enc = self.encode(mel)
+        if trace is not None:
+            trace["enc"] = enc
+            trace["picked"] = []
         cache = self.init_cache(enc)
         transcribe_tok = 50260 + c["n_lang"]
         notime = transcribe_tok + 4
@@ -268,6 +277,8 @@ class SynthWhisper:
         first_logits = logits.copy()
         logits = logits.copy()
         logits[:, EOT] = -np.inf
+        if trace is not None:
+            trace["picked"].append(logits.copy())
         nxt = [self.argmax_last(logits[b]) for b in range(B)]
         out = [[] for _ in range(B)]
         done = [False] * B
@@ -288,6 +299,8 @@ class SynthWhisper:
             if step + 1 < MIN_TOKENS:
                 logits = logits.copy()
                 logits[:, EOT] = -np.inf
+            if trace is not None:
+                trace["picked"].append(logits.copy())
             nxt = [self.argmax_last(logits[b]) for b in range(B)]
         if return_logits:
             return out, first_logits, step_logits

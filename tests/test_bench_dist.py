@@ -58,3 +58,37 @@ def test_job_value_is_whole_job_aggregate():
     assert bench.max_over_ranks(3.25, None, "cpu") == 3.25
     assert bench.clip_ids(0, 2, 1, 1) == [[0, 1], [2, 3]]
     assert bench.clip_ids(1, 2, 1, 1) == [[4, 5], [6, 7]]
+
+
+def _init_rank(rank: int, world: int, port: int, q) -> None:
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    import bench
+
+    dist = bench.init_dist()
+    try:
+        job = bench.max_over_ranks(2.0 + rank, dist, "cpu")
+        q.put((rank, dist.get_backend(), job))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_group_is_gloo_not_rccl():
+    """The bench's own group constructor: a host (gloo) group, never NCCL/RCCL
+    (north_star 'RCCL unused')."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_init_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [o[1] for o in out] == ["gloo", "gloo"]
+    assert [o[2] for o in out] == [3.0, 3.0]
+    src = open(os.path.join(REPO, "bench.py")).read()
+    assert '"nccl"' not in src and "'nccl'" not in src
