@@ -30,6 +30,17 @@ constexpr int kEOT = 50257;
 // attention scores scaled by 1/sqrt(64) * log2(e) (attention.rs:262): the
 // softmax runs in base 2, one v_exp_f32 (2^x) per exponential
 constexpr float kEaQScale = 0.125f * 1.4426950408889634f;
+// Operand scales of the f16-pair MFMAs (the MFMAs flush f16 subnormal inputs,
+// wq4_device.hpp split_act): q / 8 (base 2), k and v enter as x * 2^5 (|x| <
+// 2047), the softmax weights p in (0, 1] as p * 2^15 (<= 32768 < 65504); the
+// scores come out x 2^10 and the output x 2^20 -- undone in f32, exactly.
+constexpr float kQKScale = 32.0f, kSInv = 1.0f / 1024.0f;
+constexpr float kPScale = 32768.0f, kPVInv = 1.0f / (32768.0f * 32.0f);
+// the conv front-end: input x 2^4, weights x 2^10 (|w| < 64), product x 2^-14
+constexpr float kCvAScale = 16.0f, kCvBScale = 1024.0f, kCvInv = 1.0f / (16.0f * 1024.0f);
+// logits: hidden rows as GEMM activations (x 2^4), the f16-pair table x 2^8
+// (|e| < 255), logits x 2^-12
+constexpr float kEmbScale = 256.0f, kLgInv = 1.0f / (16.0f * 256.0f);
 
 using wq4::kLnMaxV;
 using wq4::wave_sum;
@@ -50,114 +61,15 @@ using wq4::split_f16;
 
 
 
-// ------------------------------------------------- encoder attention --
-// One workgroup = 4 waves = 128 queries of one (clip, head); each wave owns
-// 32 queries and sweeps all keys in 32-key tiles staged in LDS.  Both
-// products are computed transposed (S^T = K Q^T, O^T = V^T P^T) so that a
-// lane owns one query: the online-softmax statistics are lane-local (plus
-// one swap with lane ^ 32).  Scores use q / 8 (exact power-of-two scaling of
-// attention.rs:266-267's division).
-template <int NS>
-__global__ __launch_bounds__(256) void encoder_attention_kernel(const float* __restrict__ qkv, int T, int H,
-                                                                _Float16* __restrict__ tiled) {
-  __shared__ float ks[32 * 65];
-  __shared__ float vs[32 * 64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ql = lane & 31, h = lane >> 5;
-  const int head = blockIdx.y, b = blockIdx.z;
-  const int D = H * 64, ld = 3 * D;
-  const float* base = qkv + (size_t)b * T * ld;
-  const int q = blockIdx.x * 128 + wave * 32 + ql;
-
-  float qv[32];
-#pragma unroll
-  for (int s = 0; s < 32; ++s) qv[s] = q < T ? base[(size_t)q * ld + head * 64 + 2 * s + h] * 0.125f : 0.0f;
-
-  float m = -INFINITY, l = 0.0f;
-  floatx16 o0, o1;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    o0[i] = 0.0f;
-    o1[i] = 0.0f;
-  }
-  const int ntile = (T + 31) / 32;
-  for (int kt = 0; kt < ntile; ++kt) {
-    const int key0 = kt * 32;
-    {
-      const int key = tid >> 3, d0 = (tid & 7) * 8;
-      const bool ok = key0 + key < T;
-      const float* kr = base + (size_t)(key0 + key) * ld + D + head * 64 + d0;
-#pragma unroll
-      for (int j = 0; j < 8; j += 4) {
-        floatx4 kv4 = ok ? *reinterpret_cast<const floatx4*>(kr + j) : floatx4{0.f, 0.f, 0.f, 0.f};
-        floatx4 vv4 = ok ? *reinterpret_cast<const floatx4*>(kr + D + j) : floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          ks[key * 65 + d0 + j + e] = kv4[e];
-          vs[key * 64 + d0 + j + e] = vv4[e];
-        }
-      }
-    }
-    __syncthreads();
-    floatx16 s;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) s[i] = 0.0f;
-#pragma unroll
-    for (int st = 0; st < 32; ++st) s = mfma_f32(ks[ql * 65 + 2 * st + h], qv[st], s);
-    float mx = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int key = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-      if (key >= T) s[i] = -INFINITY;
-      mx = fmaxf(mx, s[i]);
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = expf(m - mn);
-    float rs = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      s[i] = expf(s[i] - mn);
-      rs += s[i];
-    }
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mn;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      o0[i] *= alpha;
-      o1[i] *= alpha;
-    }
-#pragma unroll
-    for (int st = 0; st < 16; ++st) {
-      const int key = (st & 3) + 8 * (st >> 2) + 4 * h;
-      o0 = mfma_f32(vs[key * 64 + ql], s[st], o0);
-      o1 = mfma_f32(vs[key * 64 + 32 + ql], s[st], o1);
-    }
-    __syncthreads();
-  }
-  if (q < T) {
-    const int row = b * T + q;
-    const int kbp = kbp_of(D);
-    const float inv = 1.0f / l;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 8 * g + 4 * h;
-      atile_store4<NS>(tiled, row, head * 64 + d, kbp, o0[4 * g] * inv, o0[4 * g + 1] * inv, o0[4 * g + 2] * inv,
-                       o0[4 * g + 3] * inv);
-      atile_store4<NS>(tiled, row, head * 64 + 32 + d, kbp, o1[4 * g] * inv, o1[4 * g + 1] * inv,
-                       o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
-    }
-  }
-}
-
 // ------------------------------------ encoder attention, f16x2 MFMA --
-// Same contract as encoder_attention_kernel (attention.rs:243-298,
-// non-causal), products on v_mfma_f32_32x32x16_f16 with every operand an
+// Encoder self-attention (attention.rs:243-298, non-causal; scores use q / 8,
+// an exact power-of-two scaling of attention.rs:266-267's division), flash
+// style: products on v_mfma_f32_32x32x16_f16 with every operand an
 // exact-to-2^-22 f16 pair (x = hi + lo; hi*hi + lo*hi + hi*lo, f32
-// accumulation -- the arithmetic of the Q4 GEMMs), 3 MFMAs per product
-// instead of the f32 MFMA's 16x slower rate.  Workgroup = 4 waves x 32
-// queries of one (clip, head); 64-key tiles of K and V are converted to f16
+// accumulation -- the arithmetic of the Q4 GEMMs).  Both products are
+// computed transposed (S^T = K Q^T, O^T = V^T P^T) so that a lane owns one
+// query and the online-softmax statistics are lane-local.  Workgroup = 8
+// waves x 32 queries of one (clip, head); 64-key tiles of K and V are converted to f16
 // pairs into LDS (row stride 72 halves: conflict-free b128 and transposed
 // reads), the next tile's f32 loads in flight meanwhile.
 //   S^T = K Q^T   A = K (m = key, k = dim) ds_read_b128; B = Q^T from registers
@@ -203,7 +115,7 @@ __global__ __launch_bounds__(64 * NW) void encoder_attention_f16_kernel(const fl
         // softmax exponentials are single v_exp_f32 (2^x) instructions
         const float v = q < T ? (j < 4 ? x0[j] : x1[j - 4]) * kEaQScale : 0.0f;
         _Float16 a, c;
-        split_f16(v, a, c);
+        split_f16(v * kQKScale, a, c);
         hi[j] = a;
         lo[j] = c;
       }
@@ -231,10 +143,10 @@ __global__ __launch_bounds__(64 * NW) void encoder_attention_f16_kernel(const fl
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
       _Float16 a, c;
-      split_f16(kreg[i >> 2][i & 3], a, c);
+      split_f16(kreg[i >> 2][i & 3] * kQKScale, a, c);
       kh[i >> 3][i & 7] = a;
       kl[i >> 3][i & 7] = c;
-      split_f16(vreg[i >> 2][i & 3], a, c);
+      split_f16(vreg[i >> 2][i & 3] * kQKScale, a, c);
       vh[i >> 3][i & 7] = a;
       vl[i >> 3][i & 7] = c;
     }
@@ -294,12 +206,12 @@ __global__ __launch_bounds__(64 * NW) void encoder_attention_f16_kernel(const fl
         mx = fmaxf(mx, st[i]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);  // exp2(-inf) = 0
+      const float mn = fmaxf(m, mx);  // scores (and m) carry the 2^10 operand scale
+      const float alpha = __builtin_amdgcn_exp2f((m - mn) * kSInv);  // exp2(-inf) = 0
       float rs = 0.0f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        st[i] = __builtin_amdgcn_exp2f(st[i] - mn);
+        st[i] = __builtin_amdgcn_exp2f((st[i] - mn) * kSInv);
         rs += st[i];
       }
       rs += __shfl_xor(rs, 32, 64);
@@ -310,14 +222,17 @@ __global__ __launch_bounds__(64 * NW) void encoder_attention_f16_kernel(const fl
         o[0][i] *= alpha;
         o[1][i] *= alpha;
       }
-      // P^T operands: MFMA t takes accumulator registers 8 t .. 8 t + 7
+      // P^T operands: MFMA t takes accumulator registers 8 t .. 8 t + 7.
+      // p in (0, 1] is split at p * 2^15 (exact scaling; undone at the end)
+      // so that the lo part of a small p stays a normal f16: 22 bits for
+      // every p >= 2^-18 instead of an absolute 2^-24 floor
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         half8 ph, pl;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           _Float16 a, c;
-          split_f16(st[8 * t + j], a, c);
+          split_f16(st[8 * t + j] * kPScale, a, c);
           ph[j] = a;
           pl[j] = c;
         }
@@ -343,7 +258,7 @@ __global__ __launch_bounds__(64 * NW) void encoder_attention_f16_kernel(const fl
   if (q < T) {
     const int row = b * T + q;
     const int kbp = kbp_of(D);
-    const float inv = 1.0f / l;
+    const float inv = (1.0f / l) * kPVInv;  // exact power-of-two rescale of 1 / l
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -357,34 +272,11 @@ __global__ __launch_bounds__(64 * NW) void encoder_attention_f16_kernel(const fl
 
 hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Float16* tiled, int ns,
                                     hipStream_t st) {
-  const dim3 grid((T + 127) / 128, H, B), block(256);
-  static const bool f32_mfma = [] {  // WA_ENC_ATTN_F32=1: the f32-MFMA kernel (A/B, diagnostics)
-    const char* e = getenv("WA_ENC_ATTN_F32");
-    return e && atoi(e) != 0;
-  }();
-  if (f32_mfma) {
-    if (ns == 2)
-      hipLaunchKernelGGL((encoder_attention_kernel<2>), grid, block, 0, st, qkv, T, H, tiled);
-    else
-      hipLaunchKernelGGL((encoder_attention_kernel<1>), grid, block, 0, st, qkv, T, H, tiled);
-  } else {
-    static const int nw = [] {  // WA_ENC_ATTN_WAVES = 4 or 8 (32 queries per wave)
-      const char* e = getenv("WA_ENC_ATTN_WAVES");
-      return e && atoi(e) == 4 ? 4 : 8;
-    }();
-    const dim3 g2((T + 32 * nw - 1) / (32 * nw), H, B);
-    if (nw == 8) {
-      if (ns == 2)
-        hipLaunchKernelGGL((encoder_attention_f16_kernel<2, 8>), g2, dim3(512), 0, st, qkv, T, H, tiled);
-      else
-        hipLaunchKernelGGL((encoder_attention_f16_kernel<1, 8>), g2, dim3(512), 0, st, qkv, T, H, tiled);
-    } else {
-      if (ns == 2)
-        hipLaunchKernelGGL((encoder_attention_f16_kernel<2, 4>), g2, dim3(256), 0, st, qkv, T, H, tiled);
-      else
-        hipLaunchKernelGGL((encoder_attention_f16_kernel<1, 4>), g2, dim3(256), 0, st, qkv, T, H, tiled);
-    }
-  }
+  const dim3 g2((T + 255) / 256, H, B);  // 8 waves x 32 queries
+  if (ns == 2)
+    hipLaunchKernelGGL((encoder_attention_f16_kernel<2, 8>), g2, dim3(512), 0, st, qkv, T, H, tiled);
+  else
+    hipLaunchKernelGGL((encoder_attention_f16_kernel<1, 8>), g2, dim3(512), 0, st, qkv, T, H, tiled);
   return hipGetLastError();
 }
 
@@ -571,87 +463,7 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
 // ------------------------------------------------------ conv + GELU --
 // out[b, t, n] = gelu(bias[n] + sum_{kk, c} in(b, c, t*S + kk - 1) W[n, c, kk])
 // (+ pos[t, n]).  GEMM view: rows (b, t), cols n, K = 3C (k = kk*C + c, the
-// reference's im2col order, layers.rs:92-121).  Workgroup tile 128 x 128,
-// 4 waves of 64 x 64, K chunks of 32 staged [k][m] / [k][n] in LDS.
-__global__ __launch_bounds__(256) void conv_gelu_kernel(const float* __restrict__ in, long in_bs, long in_cs,
-                                                        long in_ts, int B, int C, int T_in, int S,
-                                                        const float* __restrict__ wt, const float* __restrict__ bias,
-                                                        const float* __restrict__ pos, int N, float* __restrict__ out,
-                                                        int T_out) {
-  __shared__ float as[32][128 + 4];
-  __shared__ float bs[32][128 + 4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int M = B * T_out, K = 3 * C;
-  const int m0 = blockIdx.x * 128, n0 = blockIdx.y * 128;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[a][c][i] = 0.0f;
-
-  for (int kc = 0; kc < K; kc += 32) {
-    // stage A: 32 k x 128 m (im2col gather), B: 32 k x 128 n
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int e = it * 256 + tid;
-      const int kl = e >> 7, ml = e & 127;
-      const int k = kc + kl, m = m0 + ml;
-      float v = 0.0f;
-      if (k < K && m < M) {
-        const int kk = k / C, c = k - kk * C;
-        const int bb = m / T_out, t = m - bb * T_out;
-        const int ti = t * S + kk - 1;
-        if (ti >= 0 && ti < T_in) v = in[bb * in_bs + c * in_cs + (long)ti * in_ts];
-      }
-      as[kl][ml] = v;
-    }
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int e = it * 256 + tid;
-      const int nl = e >> 5, kl = e & 31;
-      const int k = kc + kl, n = n0 + nl;
-      bs[kl][nl] = (k < K && n < N) ? wt[(size_t)n * K + k] : 0.0f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int kl = 2 * s + h;
-      const float a0 = as[kl][wm + r], a1 = as[kl][wm + 32 + r];
-      const float b0 = bs[kl][wn + r], b1 = bs[kl][wn + 32 + r];
-      acc[0][0] = mfma_f32(a0, b0, acc[0][0]);
-      acc[0][1] = mfma_f32(a0, b1, acc[0][1]);
-      acc[1][0] = mfma_f32(a1, b0, acc[1][0]);
-      acc[1][1] = mfma_f32(a1, b1, acc[1][1]);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int m = m0 + wm + 32 * a + (i & 3) + 8 * (i >> 2) + 4 * h;
-        const int n = n0 + wn + 32 * c + r;
-        if (m < M && n < N) {
-          float v = wq4::gelu_tanh(acc[a][c][i] + bias[n]);
-          if (pos) v = v + pos[(size_t)(m % T_out) * N + n];
-          out[(size_t)m * N + n] = v;
-        }
-      }
-}
-
-// The same conv1d + GELU (+ positional add) on f16 MFMA: A (im2col rows)
-// and B (weights [N][3C]) staged per 32-k step as exact-to-2^-22 f16 pairs,
-// v_mfma_f32_32x32x16_f16 with three products per term (the arithmetic of the
-// Q4 GEMMs).  Thread stages 4 consecutive k of one row: one float4 load when
-// the input is channel-contiguous (conv2: in_cs == 1), four scalars
-// otherwise (conv1 reads the mel [n_mels][3000] layout).  LDS row stride 40
-// halves: conflict-free b128 fragment reads.
+// reference's im2col order, layers.rs:92-121).
 constexpr int kCvLd = 40;
 template <int NS>
 __global__ __launch_bounds__(256) void conv_gelu_f16_kernel(const float* __restrict__ in, long in_bs, long in_cs,
@@ -674,12 +486,12 @@ __global__ __launch_bounds__(256) void conv_gelu_f16_kernel(const float* __restr
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[a][c][i] = 0.0f;
-  auto put = [&](_Float16 (&dst)[NS][128 * kCvLd], int row, int kl, floatx4 v) {
+  auto put = [&](_Float16 (&dst)[NS][128 * kCvLd], int row, int kl, floatx4 v, float scale) {
     ea_half4 hi, lo;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       _Float16 a, b;
-      split_f16(v[j], a, b);
+      split_f16(v[j] * scale, a, b);
       hi[j] = a;
       lo[j] = b;
     }
@@ -709,7 +521,7 @@ __global__ __launch_bounds__(256) void conv_gelu_f16_kernel(const float* __restr
           }
         }
       }
-      put(as, ml, kl, v);
+      put(as, ml, kl, v, kCvAScale);
     }
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
@@ -718,7 +530,7 @@ __global__ __launch_bounds__(256) void conv_gelu_f16_kernel(const float* __restr
       const int n = n0 + nl, k = kc + kl;
       const floatx4 v = (n < N && k + 3 < K) ? *reinterpret_cast<const floatx4*>(wt + (size_t)n * K + k)
                                              : floatx4{0.f, 0.f, 0.f, 0.f};
-      put(bs, nl, kl, v);
+      put(bs, nl, kl, v, kCvBScale);
     }
     __syncthreads();
 #pragma unroll
@@ -754,7 +566,7 @@ __global__ __launch_bounds__(256) void conv_gelu_f16_kernel(const float* __restr
         const int m = m0 + wm + 32 * a + (i & 3) + 8 * (i >> 2) + 4 * lh;
         const int n = n0 + wn + 32 * c + l32;
         if (m < M && n < N) {
-          float v = wq4::gelu_tanh(acc[a][c][i] + bias[n]);
+          float v = wq4::gelu_tanh(acc[a][c][i] * kCvInv + bias[n]);
           if (pos) v = v + pos[(size_t)(m % T_out) * N + n];
           out[(size_t)m * N + n] = v;
         }
@@ -764,18 +576,11 @@ __global__ __launch_bounds__(256) void conv_gelu_f16_kernel(const float* __restr
 hipError_t launch_conv_gelu(const float* in, long in_bs, long in_cs, long in_ts, int B, int C, int T_in,
                             int stride, const float* w_t, const float* bias, const float* pos, int N, float* out,
                             hipStream_t st) {
+  if (C % 4 != 0) return hipErrorInvalidValue;  // float4 channel staging (n_mels 80 / 128, D)
   const int T_out = (T_in + 2 - 3) / stride + 1;
   const dim3 grid((B * T_out + 127) / 128, (N + 127) / 128), block(256);
-  static const bool f32_mfma = [] {  // WA_CONV_F32=1: the f32-MFMA kernel (A/B, diagnostics)
-    const char* e = getenv("WA_CONV_F32");
-    return e && atoi(e) != 0;
-  }();
-  if (f32_mfma || C % 4 != 0 || (3 * C) % 4 != 0)
-    hipLaunchKernelGGL(conv_gelu_kernel, grid, block, 0, st, in, in_bs, in_cs, in_ts, B, C, T_in, stride, w_t, bias,
-                       pos, N, out, T_out);
-  else
-    hipLaunchKernelGGL(conv_gelu_f16_kernel<2>, grid, block, 0, st, in, in_bs, in_cs, in_ts, B, C, T_in, stride, w_t,
-                       bias, pos, N, out, T_out);
+  hipLaunchKernelGGL(conv_gelu_f16_kernel<2>, grid, block, 0, st, in, in_bs, in_cs, in_ts, B, C, T_in, stride, w_t,
+                     bias, pos, N, out, T_out);
   return hipGetLastError();
 }
 
@@ -958,17 +763,13 @@ hipError_t launch_argmax_step(const float* logits, int B, int V, int min_tokens,
 // ------------------------------------------------ logits + greedy pick --
 // Decode step (B <= 32 clips): logits[b, v] = h[b] . E[v] (decoder.rs:289-292)
 // fused with the greedy argmax (whisper.rs:119-124, 131-138) -- the logits
-// never reach HBM.  Workgroup = 4 waves x 32 vocabulary rows; per 256-wide k
-// chunk the hidden rows are staged in LDS and the next chunk's embedding
-// float4s are already in flight in registers (the 265 MB f32 embedding is
-// the step's largest stream).  Each workgroup leaves one (max, index)
-// candidate per clip; the last-arriving workgroup (agent-scope ticket,
-// write-through partials: cdna_hip_programming.md Guideline 16 R1) reduces
-// them.  (value, index) is compared lexicographically -- the largest value,
-// the LARGEST index among equal maxima -- so the result equals the
-// sequential Rust max_by scan whatever the reduction order.
-constexpr int kLgChunk = 256;
-constexpr int kLgLd = kLgChunk + 4;
+// never reach HBM (logits_argmax_f16_k32_kernel below).  Each workgroup
+// leaves one (max, index) candidate per clip; the last-arriving workgroup
+// (agent-scope ticket, write-through partials: cdna_hip_programming.md
+// Guideline 16 R1) reduces them.  (value, index) is compared
+// lexicographically -- the largest value, the LARGEST index among equal
+// maxima -- so the result equals the sequential Rust max_by scan whatever the
+// reduction order.
 
 __device__ __forceinline__ void better_pair(float& bv, int& bi, float v, int i) {
   if (v > bv || (v == bv && i > bi)) {
@@ -979,7 +780,7 @@ __device__ __forceinline__ void better_pair(float& bv, int& bi, float v, int i) 
 
 // Greedy pick of a workgroup's 32 x 128 logits block lg[clip][kLgPickLd]
 // (already masked), then the last-arriving workgroup's pick over all
-// workgroups' candidates (see logits_argmax_kernel).
+// workgroups' candidates.
 constexpr int kLgPickLd = 132;
 __device__ __forceinline__ void pick_from_lds(const float* lg, int B, int V, float* __restrict__ pval,
                                               int* __restrict__ pidx, int* __restrict__ counter,
@@ -1041,171 +842,24 @@ __device__ __forceinline__ void pick_from_lds(const float* lg, int B, int V, flo
   }
 }
 
-__global__ __launch_bounds__(256) void logits_argmax_kernel(const float* __restrict__ hid, int B, int D, long ldh,
-                                                            const float* __restrict__ emb, int V, int min_tokens,
-                                                            const DecodeState* __restrict__ state,
-                                                            float* __restrict__ pval, int* __restrict__ pidx,
-                                                            int* __restrict__ counter, int* __restrict__ out_tok) {
-  __shared__ __attribute__((aligned(16))) float hs[32 * kLgLd];
-  __shared__ int ticket;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int n = blockIdx.x * 128 + wave * 32 + r;
-  const float* er = emb + (size_t)(n < V ? n : V - 1) * D;
-  const int nch = (D + kLgChunk - 1) / kLgChunk;
-  floatx16 acc;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
-  floatx4 ec[kLgChunk / 8], en[kLgChunk / 8];
-  auto load_e = [&](floatx4 (&e)[kLgChunk / 8], int kc) {
-#pragma unroll
-    for (int j = 0; j < kLgChunk / 8; ++j) {
-      const int k = kc + 8 * j + 4 * h;
-      e[j] = *reinterpret_cast<const floatx4*>(er + (k < D ? k : 0));
-    }
-  };
-  load_e(ec, 0);
-  for (int c = 0; c < nch; ++c) {
-    const int kc = c * kLgChunk;
-    if (c + 1 < nch) load_e(en, kc + kLgChunk);
-    __syncthreads();
-    for (int e = tid; e < 32 * (kLgChunk / 4); e += 256) {
-      const int row = e / (kLgChunk / 4), k4 = (e % (kLgChunk / 4)) * 4;
-      const floatx4 v = (row < B && kc + k4 < D) ? *reinterpret_cast<const floatx4*>(hid + (size_t)row * ldh + kc + k4)
-                                                 : floatx4{0.f, 0.f, 0.f, 0.f};
-      *reinterpret_cast<floatx4*>(&hs[row * kLgLd + k4]) = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kLgChunk / 8; ++j) {
-      const floatx4 a = *reinterpret_cast<const floatx4*>(&hs[r * kLgLd + 8 * j + 4 * h]);
-      const bool kin = kc + 8 * j < D;  // D % 8 == 0
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc = mfma_f32(kin ? a[s] : 0.0f, ec[j][s], acc);
-    }
-    if (c + 1 < nch) {
-#pragma unroll
-      for (int j = 0; j < kLgChunk / 8; ++j) ec[j] = en[j];
-    }
-  }
-  // this workgroup's 32 x 128 logits -> LDS, then (max, index) per clip
-  __syncthreads();
-  float* lg = hs;  // [32 rows][128 + 4]
-  const int suppress = state->step + 1 < min_tokens;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
-    float v = acc[i];
-    if (n >= V || (suppress && n == kEOT)) v = -INFINITY;
-    lg[row * kLgPickLd + wave * 32 + r] = v;
-  }
-  pick_from_lds(lg, B, V, pval, pidx, counter, out_tok, &ticket);
-}
-
-// The same on f16 MFMA: the embedding as exact-to-2^-22 f16 pairs
-// (emb2 [V][NS][D], launch_enc_planes of the f32 table, prepared once),
-// E = hi + lo, and the hidden rows split likewise; three 32x32x16 f16
-// MFMAs per product (hi*hi + lo*hi + hi*lo) with f32 accumulation, 16x
-// the f32 MFMA rate, so the 265 MB table streams at HBM speed.  Workgroup =
-// 4 waves x 32 vocabulary rows (m), the 32 clips as n; per 128-dim chunk
-// the hidden rows are staged in LDS as f16 pairs and the next chunk's
-// embedding fragments are already in flight in registers.
 constexpr int kLg2Chunk = 128;
 constexpr int kLg2Ld = kLg2Chunk + 8;  // halves
 
-template <int NS>
-__global__ __launch_bounds__(256) void logits_argmax_f16_kernel(const float* __restrict__ hid, int B, int D, long ldh,
-                                                                const _Float16* __restrict__ emb2, int V,
-                                                                int min_tokens, const DecodeState* __restrict__ state,
-                                                                float* __restrict__ pval, int* __restrict__ pidx,
-                                                                int* __restrict__ counter, int* __restrict__ out_tok) {
-  __shared__ __attribute__((aligned(16))) _Float16 hsh[NS][32 * kLg2Ld];
-  __shared__ __attribute__((aligned(16))) float lg[32 * kLgPickLd];
-  __shared__ int ticket;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, lh = lane >> 5;
-  const int v0 = blockIdx.x * 128 + wave * 32;
-  const int vrow = v0 + r < V ? v0 + r : V - 1;
-  const _Float16* er = emb2 + (size_t)vrow * NS * D;
-  const int nch = (D + kLg2Chunk - 1) / kLg2Chunk;
-  constexpr int KS = kLg2Chunk / 16;
-  floatx16 acc;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
-  half8 ec[KS][NS], en[KS][NS];
-  auto load_e = [&](half8 (&e)[KS][NS], int kc) {
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int p = 0; p < NS; ++p) {
-        const int k = kc + 16 * ks + 8 * lh;
-        e[ks][p] = *reinterpret_cast<const half8*>(er + (size_t)p * D + (k < D ? k : 0));
-      }
-  };
-  load_e(ec, 0);
-  for (int c = 0; c < nch; ++c) {
-    const int kc = c * kLg2Chunk;
-    if (c + 1 < nch) load_e(en, kc + kLg2Chunk);
-    __syncthreads();
-    for (int e = tid; e < 32 * (kLg2Chunk / 4); e += 256) {  // (row, 4 dims) -> f16 pairs
-      const int row = e / (kLg2Chunk / 4), k4 = (e % (kLg2Chunk / 4)) * 4;
-      const floatx4 x = (row < B && kc + k4 < D) ? *reinterpret_cast<const floatx4*>(hid + (size_t)row * ldh + kc + k4)
-                                                 : floatx4{0.f, 0.f, 0.f, 0.f};
-      ea_half4 hi, lo;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        _Float16 a, b;
-        split_f16(x[j], a, b);
-        hi[j] = a;
-        lo[j] = b;
-      }
-      *reinterpret_cast<ea_half4*>(&hsh[0][row * kLg2Ld + k4]) = hi;
-      if constexpr (NS == 2) *reinterpret_cast<ea_half4*>(&hsh[NS - 1][row * kLg2Ld + k4]) = lo;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const bool kin = kc + 16 * ks < D;  // D % 16 == 0
-      if (kin) {
-        const half8 bh = *reinterpret_cast<const half8*>(&hsh[0][r * kLg2Ld + 16 * ks + 8 * lh]);
-        acc = ea_mfma(ec[ks][0], bh, acc);
-        if constexpr (NS == 2) {
-          const half8 bl = *reinterpret_cast<const half8*>(&hsh[1][r * kLg2Ld + 16 * ks + 8 * lh]);
-          acc = ea_mfma(ec[ks][1], bh, acc);
-          acc = ea_mfma(ec[ks][0], bl, acc);
-        }
-      }
-    }
-    if (c + 1 < nch) {
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-        for (int p = 0; p < NS; ++p) ec[ks][p] = en[ks][p];
-    }
-  }
-  // acc: m = vocab v0 + row(i), n = clip r -> lg[clip][vocab]
-  const int suppress = state->step + 1 < min_tokens;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int vl = (i & 3) + 8 * (i >> 2) + 4 * lh;
-    const int n = v0 + vl;
-    float v = acc[i];
-    if (n >= V || (suppress && n == kEOT)) v = -INFINITY;
-    lg[r * kLgPickLd + wave * 32 + vl] = v;
-  }
-  pick_from_lds(lg, B, V, pval, pidx, counter, out_tok, &ticket);
-}
-
-// 16x16x32 form of logits_argmax_f16_kernel over the fragment-tiled table
-// (launch_emb_tiled): a lane's embedding fragment is 8 dims of one of 16
-// rows, stored so that one load instruction reads 1 KiB contiguous (the row-
-// major table gave 16 rows x 64 B per instruction).  Wave = 32 vocabulary
-// rows as two 16-row m-tiles, the 32 clips as two n-tiles.
+// Tied-embedding logits of the decode step on f16 MFMA, fused with the greedy
+// pick: the embedding as exact-to-2^-22 f16 pairs E = hi + lo in a
+// fragment-tiled table (launch_emb_tiled: a lane's fragment is 8 dims of one
+// of 16 rows, one load instruction reads 1 KiB contiguous), the hidden rows
+// split likewise; three 16x16x32 f16 MFMAs per product (hi*hi + lo*hi +
+// hi*lo), f32 accumulation.  Wave = 32 vocabulary rows as two 16-row m-tiles,
+// the 32 clips as two n-tiles.  trace_out (diagnostics, null in the product
+// graph): the logits of trace_ids[clip][step + 1][0..trace_k) are written to
+// the same slots of trace_out, as the pick sees them (EOT already masked).
 template <int NS>
 __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
     const float* __restrict__ hid, int B, int D, long ldh, const _Float16* __restrict__ emb2, int V, int min_tokens,
     const DecodeState* __restrict__ state, float* __restrict__ pval, int* __restrict__ pidx, int* __restrict__ counter,
-    int* __restrict__ out_tok) {
+    int* __restrict__ out_tok, const int* __restrict__ trace_ids, float* __restrict__ trace_out, int trace_s1,
+    int trace_k) {
   __shared__ __attribute__((aligned(16))) _Float16 hsh[NS][32 * kLg2Ld];
   __shared__ __attribute__((aligned(16))) float lg[32 * kLgPickLd];
   __shared__ int ticket;
@@ -1269,7 +923,7 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         _Float16 a, b;
-        split_f16(hc[i][j], a, b);
+        wq4::split_act(hc[i][j], a, b);
         hi[j] = a;
         lo[j] = b;
       }
@@ -1316,10 +970,21 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
       for (int j = 0; j < 4; ++j) {
         const int vl = 16 * mt + 4 * lq + j;
         const int n = v0 + vl;
-        float v = acc[mt][nt][j];
+        float v = acc[mt][nt][j] * kLgInv;
         if (n >= V || (suppress && n == kEOT)) v = -INFINITY;
         lg[(16 * nt + l16) * kLgPickLd + wave * 32 + vl] = v;
       }
+  if (trace_out) {  // diagnostics only: uniform branch
+    __syncthreads();
+    const int slot = state->step + 1;
+    if (slot < trace_s1)
+      for (int e = tid; e < B * trace_k; e += 256) {
+        const int b = e / trace_k;
+        const size_t o = ((size_t)b * trace_s1 + slot) * trace_k + (e - b * trace_k);
+        const int id = trace_ids[o] - (int)blockIdx.x * 128;
+        if (id >= 0 && id < 128) trace_out[o] = lg[b * kLgPickLd + id];
+      }
+  }
   pick_from_lds(lg, B, V, pval, pidx, counter, out_tok, &ticket);
 }
 
@@ -1341,7 +1006,7 @@ __global__ __launch_bounds__(256) void emb_tiled_kernel(const float* __restrict_
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     _Float16 a = (_Float16)0.0f, b = (_Float16)0.0f;
-    if (v < V) split_f16(x[v * D + k + j], a, b);
+    if (v < V) split_f16(x[v * D + k + j] * kEmbScale, a, b);
     hi[j] = a;
     lo[j] = b;
   }
@@ -1363,28 +1028,18 @@ hipError_t launch_emb_tiled(const float* emb, int V, int D, int ns, _Float16* ou
   return hipGetLastError();
 }
 
-hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const float* emb, const _Float16* emb2,
-                                int emb2_tiled, int ns, int V, int min_tokens, const DecodeState* state, float* pval,
-                                int* pidx, int* counter, int* out_tok, hipStream_t st) {
-  if (B < 1 || B > 32 || D % 16 != 0 || !state) return hipErrorInvalidValue;
+hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const _Float16* emb2, int ns, int V,
+                                int min_tokens, const DecodeState* state, float* pval, int* pidx, int* counter,
+                                int* out_tok, const int* trace_ids, float* trace_out, int trace_s1, int trace_k,
+                                hipStream_t st) {
+  if (B < 1 || B > 32 || !emb_tiled_supported(D) || !state || !emb2) return hipErrorInvalidValue;
   const dim3 grid(logits_argmax_groups(V));
-  if (emb2 && emb2_tiled) {
-    if (!emb_tiled_supported(D)) return hipErrorInvalidValue;
-    if (ns == 2)
-      hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<2>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens,
-                         state, pval, pidx, counter, out_tok);
-    else
-      hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<1>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens,
-                         state, pval, pidx, counter, out_tok);
-  } else if (emb2 && ns == 2)
-    hipLaunchKernelGGL(logits_argmax_f16_kernel<2>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens, state,
-                       pval, pidx, counter, out_tok);
-  else if (emb2)
-    hipLaunchKernelGGL(logits_argmax_f16_kernel<1>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens, state,
-                       pval, pidx, counter, out_tok);
+  if (ns == 2)
+    hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<2>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens,
+                       state, pval, pidx, counter, out_tok, trace_ids, trace_out, trace_s1, trace_k);
   else
-    hipLaunchKernelGGL(logits_argmax_kernel, grid, dim3(256), 0, st, h, B, D, ldh, emb, V, min_tokens, state, pval,
-                       pidx, counter, out_tok);
+    hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<1>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens,
+                       state, pval, pidx, counter, out_tok, trace_ids, trace_out, trace_s1, trace_k);
   return hipGetLastError();
 }
 

@@ -87,12 +87,13 @@ hipError_t launch_argmax(const float* logits, int B, int V, int lo, int hi, int 
 // D % 8 == 0; pval / pidx: 32 * logits_argmax_groups(V) scratch each,
 // counter: one int zeroed once (re-armed by the kernel).
 int logits_argmax_groups(int V);
-// emb2 != nullptr: the f16-pair table on f16 MFMA -- fragment-tiled
-// (launch_emb_tiled) when emb2_tiled, else [V][ns][D] (launch_enc_planes of
-// emb); else the f32 table on f32 MFMA.  D % 16 == 0.
-hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const float* emb, const _Float16* emb2,
-                                int emb2_tiled, int ns, int V, int min_tokens, const DecodeState* state, float* pval,
-                                int* pidx, int* counter, int* out_tok, hipStream_t st);
+// emb2: the f16-pair table, fragment-tiled (launch_emb_tiled); D % 128 == 0.
+// trace_ids / trace_out (diagnostics; null in the product): [B][trace_s1]
+// [trace_k] -- the logits of the listed ids at slot state->step + 1.
+hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const _Float16* emb2, int ns, int V,
+                                int min_tokens, const DecodeState* state, float* pval, int* pidx, int* counter,
+                                int* out_tok, const int* trace_ids, float* trace_out, int trace_s1, int trace_k,
+                                hipStream_t st);
 // Whether the logits kernel reads a fragment-tiled table for this width.
 bool emb_tiled_supported(int D);
 // Rows of the fragment-tiled table (V padded to the kernel's 128-row groups).

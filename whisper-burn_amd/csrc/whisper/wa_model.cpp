@@ -181,7 +181,7 @@ struct DecGroup {
   wa::DecodeState* state;
   int* host_ndone = nullptr;  // pinned ring
   hipGraphExec_t graph = nullptr;
-  int graph_key = -1;
+  int64_t graph_key = -1;  // (b0, nb, eot mode, trace) the graph was captured for
 };
 
 }  // namespace
@@ -197,8 +197,7 @@ struct wa_model {
   // globals
   float *conv1_wt, *conv1_b, *conv2_wt, *conv2_b, *enc_pos, *lnp_w, *lnp_b;
   float *tok_emb, *dec_pos, *dln_w, *dln_b;
-  _Float16* tok_emb2 = nullptr;  // tied embedding as f16 pairs for the step's logits
-  int emb2_tiled = 0;            // tok_emb2 fragment-tiled (wa::launch_emb_tiled), else [V][ns][D]
+  _Float16* tok_emb2 = nullptr;  // tied embedding as fragment-tiled f16 pairs (wa::launch_emb_tiled)
   std::vector<EncLayer> enc;
   std::vector<DecLayer> dec;
   // encoder activations
@@ -215,6 +214,11 @@ struct wa_model {
   int kv_batch = 0;  // clips of the last encoder pass (enc_planes valid for [0, kv_batch))
   hipStream_t own_stream = nullptr;  // encoder / cross-K/V (graph capture needs a non-null stream)
   float timings[5] = {0, 0, 0, 0, 0};
+  // decode-step logit trace (wa_transcribe_trace; null otherwise): device
+  // [clip][trace_s1][trace_k] ids and their logits
+  const int* trace_ids = nullptr;
+  float* trace_out = nullptr;
+  int trace_s1 = 0, trace_k = 0;
   // live kernel timing (wa_profile_*)
   struct Pending {
     hipEvent_t a, b;
@@ -605,16 +609,13 @@ wq4_status alloc_activations(wa_model* m) {
     L.cache_v = f32((int64_t)B * c.n_text_ctx * Dt);
   }
   // f16-pair tied embedding for the decode step's fused logits + pick,
-  // fragment-tiled (1 KiB contiguous per load instruction) where supported
-  m->emb2_tiled = wa::emb_tiled_supported(Dt) ? 1 : 0;
-  const size_t erows = m->emb2_tiled ? (size_t)wa::emb_tiled_rows(c.n_vocab) : (size_t)c.n_vocab;
+  // fragment-tiled (1 KiB contiguous per load instruction)
+  if (!wa::emb_tiled_supported(Dt)) return fail(WQ4_EINVAL, "n_text_state must be a multiple of 128");
+  const size_t erows = (size_t)wa::emb_tiled_rows(c.n_vocab);
   m->tok_emb2 = d.alloc<_Float16>(erows * m->ns * Dt);
   if (!m->tok_emb2) return fail(WQ4_ENOMEM, "embedding plane allocation failed");
   m->bytes += erows * m->ns * Dt * 2;
-  if (m->emb2_tiled)
-    WA_HIP(wa::launch_emb_tiled(m->tok_emb, c.n_vocab, Dt, m->ns, m->tok_emb2, nullptr));
-  else
-    WA_HIP(wa::launch_enc_planes(m->tok_emb, c.n_vocab, Dt, m->ns, m->tok_emb2, nullptr));
+  WA_HIP(wa::launch_emb_tiled(m->tok_emb, c.n_vocab, Dt, m->ns, m->tok_emb2, nullptr));
   // cross-attention scratch, sized for the largest plan over 1..4B rows
   const int HP = (c.n_text_head + 15) / 16 * 16;
   size_t xpart = 0;
@@ -856,8 +857,10 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
   // position of every clip (decoder.rs:289-292, 342-343)
   WA_WQ4(wq4_layernorm(g.xd, m->dln_w, m->dln_b, rows, D, WQ4_PREC_F16X2, nullptr, g.hid, st));
   if (fused_pick(g, Tq, state)) {  // decode step: logits + greedy pick in one kernel, into next_tok
-    WA_HIP(wa::launch_logits_argmax(g.hid, B, D, D, m->tok_emb, m->tok_emb2, m->emb2_tiled, m->ns, c.n_vocab,
-                                    kMinTokens, state, g.lg_val, g.lg_idx, g.lg_ctr, g.next_tok, st));
+    const size_t tofs = (size_t)g.b0 * m->trace_s1 * m->trace_k;
+    WA_HIP(wa::launch_logits_argmax(g.hid, B, D, D, m->tok_emb2, m->ns, c.n_vocab, kMinTokens, state, g.lg_val,
+                                    g.lg_idx, g.lg_ctr, g.next_tok, m->trace_out ? m->trace_ids + tofs : nullptr,
+                                    m->trace_out ? m->trace_out + tofs : nullptr, m->trace_s1, m->trace_k, st));
     return WQ4_OK;
   }
   WA_HIP(wa::launch_logits(g.hid + (size_t)(Tq - 1) * D, B, D, (int64_t)Tq * D, m->tok_emb, c.n_vocab, g.logits,
@@ -931,7 +934,9 @@ wq4_status prompt_group(wa_model* m, DecGroup& g, int lang_token, hipStream_t st
 
 // Capture (once per group size / eot mode) the step graph of group g.
 wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
-  const int key = g.nb * 2 + (eot_stop ? 1 : 0);
+  // everything the captured step bakes in: the clip range (self-KV and
+  // encoder-plane offsets), the EOT mode and the trace buffers
+  const int64_t key = (((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0);
   if (g.graph && g.graph_key == key) return WQ4_OK;
   if (g.graph) {
     (void)hipGraphExecDestroy(g.graph);
@@ -1297,6 +1302,27 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
   return WQ4_OK;
 }
 
+wq4_status wa_transcribe_trace(wa_model* m, const float* mel_dev, int n_clips, int lang_token, int max_tokens,
+                               int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out, const int32_t* trace_ids_dev,
+                               int trace_k, float* trace_out_dev, void* stream) {
+  if (!m || !trace_ids_dev || !trace_out_dev || trace_k < 1) return fail(WQ4_EINVAL, "bad trace arguments");
+  m->trace_ids = trace_ids_dev;
+  m->trace_out = trace_out_dev;
+  m->trace_s1 = max_tokens + 1;
+  m->trace_k = trace_k;
+  const wq4_status s = wa_transcribe(m, mel_dev, n_clips, lang_token, max_tokens, eot_stop, tokens_out,
+                                     n_tokens_out, stream);
+  m->trace_ids = nullptr;
+  m->trace_out = nullptr;
+  m->trace_s1 = m->trace_k = 0;
+  for (DecGroup& g : m->groups) {  // the trace graphs bake in the caller's buffers: never replay them again
+    if (g.graph) (void)hipGraphExecDestroy(g.graph);
+    g.graph = nullptr;
+    g.graph_key = -1;
+  }
+  return s;
+}
+
 wq4_status wa_probe_kernels(wa_model* m, int n_clips, int iters, double* out) {
   if (!m || !out) return fail(WQ4_EINVAL, "null argument");
   if (n_clips < 1 || n_clips > m->bmax || iters < 1) return fail(WQ4_EINVAL, "bad n_clips / iters");
@@ -1366,6 +1392,88 @@ wq4_status wa_xattn_check(int device, const float* q_dev, const uint8_t* wk_dev,
   WA_HIP(wa::launch_xattn(q_dev, wk_dev, wv_dev, bv_dev, weight_type, planes, n_clips, Tq, T, H, D, qt, part, tiled,
                           ns, nullptr));
   WA_HIP(wa::launch_untile(tiled, R, D, ns, out_dev, nullptr));
+  WA_HIP(hipDeviceSynchronize());
+  return WQ4_OK;
+}
+
+wq4_status wa_encoder_attention_check(int device, const float* qkv_dev, int n_clips, int T, int H, wq4_precision prec,
+                                      float* out_dev) {
+  if (!qkv_dev || !out_dev) return fail(WQ4_EINVAL, "null argument");
+  if (n_clips < 1 || T < 1 || H < 1) return fail(WQ4_EINVAL, "bad sizes");
+  const int D = 64 * H, ns = prec == WQ4_PREC_F16 ? 1 : 2;
+  const int64_t R = (int64_t)n_clips * T;
+  WA_HIP(hipSetDevice(device));
+  Dev d;
+  const size_t tb = wq4_atiled_bytes(R, D, prec);
+  auto* tiled = d.alloc<_Float16>(tb / 2);
+  if (!tiled) return fail(WQ4_ENOMEM, "allocation failed");
+  WA_HIP(hipMemset(tiled, 0, tb));
+  WA_HIP(wa::launch_encoder_attention(qkv_dev, n_clips, T, H, tiled, ns, nullptr));
+  WA_HIP(wa::launch_untile(tiled, (int)R, D, ns, out_dev, nullptr));
+  WA_HIP(hipDeviceSynchronize());
+  return WQ4_OK;
+}
+
+wq4_status wa_self_attention_check(int device, const float* qkv_dev, float* cache_k_dev, float* cache_v_dev,
+                                   int n_clips, int Tq, int H, int ctx, int kv_len, wq4_precision prec,
+                                   float* out_dev) {
+  if (!qkv_dev || !cache_k_dev || !cache_v_dev || !out_dev) return fail(WQ4_EINVAL, "null argument");
+  if (n_clips < 1 || Tq < 1 || Tq > 4 || H < 1 || ctx < 1 || ctx > 448 || kv_len < 0 || kv_len + Tq > ctx)
+    return fail(WQ4_EINVAL, "bad sizes");
+  const int D = 64 * H, ns = prec == WQ4_PREC_F16 ? 1 : 2, R = n_clips * Tq;
+  WA_HIP(hipSetDevice(device));
+  Dev d;
+  const size_t tb = wq4_atiled_bytes(R, D, prec);
+  auto* tiled = d.alloc<_Float16>(tb / 2);
+  if (!tiled) return fail(WQ4_ENOMEM, "allocation failed");
+  WA_HIP(hipMemset(tiled, 0, tb));
+  WA_HIP(wa::launch_decoder_self_attention(qkv_dev, cache_k_dev, cache_v_dev, n_clips, Tq, H, ctx, nullptr, kv_len,
+                                           tiled, ns, nullptr));
+  WA_HIP(wa::launch_untile(tiled, R, D, ns, out_dev, nullptr));
+  WA_HIP(hipDeviceSynchronize());
+  return WQ4_OK;
+}
+
+wq4_status wa_logits_argmax_check(int device, const float* hid_dev, const float* emb_dev, int n_clips, int D, int V,
+                                  int step, wq4_precision prec, int32_t* tok_dev, float* logits_dev) {
+  if (!hid_dev || !emb_dev || !tok_dev) return fail(WQ4_EINVAL, "null argument");
+  if (n_clips < 1 || n_clips > 32 || V < 1 || !wa::emb_tiled_supported(D)) return fail(WQ4_EINVAL, "bad sizes");
+  const int ns = prec == WQ4_PREC_F16 ? 1 : 2;
+  WA_HIP(hipSetDevice(device));
+  Dev d;
+  const int64_t erows = wa::emb_tiled_rows(V);
+  const int ng = wa::logits_argmax_groups(V);
+  auto* emb2 = d.alloc<_Float16>((size_t)erows * ns * D);
+  auto* st = d.alloc<wa::DecodeState>(1);
+  auto* pval = d.alloc<float>((size_t)32 * ng);
+  auto* pidx = d.alloc<int>((size_t)32 * ng);
+  auto* ctr = d.alloc<int>(1);
+  int* ids = nullptr;
+  if (logits_dev) ids = d.alloc<int>((size_t)n_clips * 2 * V);
+  if (!emb2 || !st || !pval || !pidx || !ctr || (logits_dev && !ids)) return fail(WQ4_ENOMEM, "allocation failed");
+  WA_HIP(wa::launch_emb_tiled(emb_dev, V, D, ns, emb2, nullptr));
+  // A trace writes slot state->step + 1 of [clip][2][V] (every id listed at
+  // slot 1): the state's step is then 0 and the EOT suppression of `step`
+  // (step + 1 < 3, whisper.rs:120-122) is passed through min_tokens instead.
+  const wa::DecodeState s0{0, 0, logits_dev ? 0 : step, 0};
+  const int min_tokens = !logits_dev ? kMinTokens : (step + 1 < kMinTokens ? 1 << 30 : 0);
+  WA_HIP(hipMemcpy(st, &s0, sizeof(s0), hipMemcpyHostToDevice));
+  WA_HIP(hipMemset(ctr, 0, sizeof(int)));
+  float* tr = nullptr;
+  if (logits_dev) {
+    std::vector<int> h((size_t)n_clips * 2 * V, 0);
+    for (int b = 0; b < n_clips; ++b)
+      for (int v = 0; v < V; ++v) h[((size_t)b * 2 + 1) * V + v] = v;
+    WA_HIP(hipMemcpy(ids, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    tr = d.alloc<float>((size_t)n_clips * 2 * V);
+    if (!tr) return fail(WQ4_ENOMEM, "allocation failed");
+  }
+  WA_HIP(wa::launch_logits_argmax(hid_dev, n_clips, D, D, emb2, ns, V, min_tokens, st, pval, pidx, ctr, tok_dev,
+                                  ids, tr, 2, V, nullptr));
+  if (logits_dev)
+    for (int b = 0; b < n_clips; ++b)
+      WA_HIP(hipMemcpy(logits_dev + (size_t)b * V, tr + ((size_t)b * 2 + 1) * V, (size_t)V * 4,
+                       hipMemcpyDeviceToDevice));
   WA_HIP(hipDeviceSynchronize());
   return WQ4_OK;
 }

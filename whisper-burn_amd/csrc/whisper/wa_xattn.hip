@@ -45,7 +45,17 @@ constexpr int kWtQ4 = 0, kWtF16 = 1;  // raw weight formats (wa_model wtype)
 constexpr int kTc = 16;          // keys (encoder frames) per sub-chunk
 constexpr int kMaxD = 1280;
 constexpr float kXqScale = 0.125f * 1.4426950408889634f;  // 1 / sqrt(64) * log2(e)
-constexpr int kMaxSplits = 16;  // frame ranges per query row (merge weights in xattn_out_kernel LDS)
+// Operand scales of the f16-pair MFMAs (the MFMAs flush f16 subnormal inputs:
+// wq4_device.hpp split_act), all powers of two, undone in f32 (exact):
+//   xattn_q   q rows x 2^4 (split_act), Wk x 2^12 (|w| < 16), product x 2^-16
+//   main      qt x 2^5, encoder planes x 2^5 (|x| < 2047): scores x 2^10;
+//             p in (0, 1] x 2^15: Z x 2^20
+//   out       Zn x 2^5, Wv scale d x 2^12 (d < 16): product x 2^-17
+constexpr float kWkScale = 4096.0f, kXqInv = 1.0f / (16.0f * 4096.0f);
+constexpr float kQtScale = 32.0f, kEncScale = 32.0f, kSInv = 1.0f / 1024.0f;
+constexpr float kPScale = 32768.0f, kZInv = 1.0f / (32768.0f * 32.0f);
+constexpr float kZnScale = 32.0f, kWvScale = 4096.0f, kOutInv = 1.0f / (32.0f * 4096.0f);
+constexpr int kXattnSplits = 8;  // frame ranges per query row (measured: 8 beat 4, 6, 12 and 16)
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -89,69 +99,9 @@ __device__ __forceinline__ void load_w32(const uint8_t* __restrict__ w, int K, i
 }
 
 // ------------------------------------------------------------- qt = Wk^T q --
-// grid (H, D / 64, ceil(R / 32)), 256 threads: 64 columns of one head for up
-// to 32 rows.  qt: [R][NS][HP][D] f16 planes (rows of padded heads h >= H
-// are never written: zeroed once at allocation).  Thread (row, 8 columns).
-template <int NS, int WK>
-__global__ __launch_bounds__(256) void xattn_q_kernel(const float* __restrict__ q, int R, int D,
-                                                      const uint8_t* __restrict__ wk, int HP,
-                                                      _Float16* __restrict__ qt) {
-  __shared__ __attribute__((aligned(16))) float wt[64][64 + 4];
-  __shared__ float qs[32][65];
-  const int h = blockIdx.x, c0 = blockIdx.y * 64, r0 = blockIdx.z * 32, tid = threadIdx.x;
-  float qv[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int i = tid + k * 256, row = i >> 6, d = i & 63;
-    qv[k] = r0 + row < R ? q[(size_t)(r0 + row) * D + h * 64 + d] : 0.0f;
-  }
-  if (tid < 128) {  // 64 rows x 2 blocks of 32 columns
-    const int d = tid >> 1, blk = tid & 1;
-    float v[32];
-    load_w32<WK>(wk, D, h * 64 + d, (c0 >> 5) + blk, v);
-#pragma unroll
-    for (int i = 0; i < 32; i += 4)
-      *reinterpret_cast<floatx4*>(&wt[d][blk * 32 + i]) = floatx4{v[i], v[i + 1], v[i + 2], v[i + 3]};
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int i = tid + k * 256;
-    qs[i >> 6][i & 63] = qv[k];
-  }
-  __syncthreads();
-  const int rr = tid >> 3, cc = (tid & 7) * 8;
-  float acc[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
-#pragma unroll 4
-  for (int d = 0; d < 64; ++d) {
-    const floatx4 w0 = *reinterpret_cast<const floatx4*>(&wt[d][cc]);
-    const floatx4 w1 = *reinterpret_cast<const floatx4*>(&wt[d][cc + 4]);
-    const float qq = qs[rr][d];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      acc[i] = fmaf(qq, w0[i], acc[i]);
-      acc[4 + i] = fmaf(qq, w1[i], acc[4 + i]);
-    }
-  }
-  const int r = r0 + rr;
-  if (r < R) {
-    half8 hi, lo;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      _Float16 x, y;
-      // / sqrt(64) (attention.rs:262) * log2(e): scores in base-2 units, so
-      // the softmax uses v_exp_f32 (2^x) directly
-      split_f16(acc[i] * kXqScale, x, y);
-      hi[i] = x;
-      lo[i] = y;
-    }
-    *reinterpret_cast<half8*>(qt + (((size_t)r * NS + 0) * HP + h) * D + c0 + cc) = hi;
-    if (NS == 2) *reinterpret_cast<half8*>(qt + (((size_t)r * NS + 1) * HP + h) * D + c0 + cc) = lo;
-  }
-}
-
-// MFMA form of xattn_q_kernel, same grid, 128 threads: out[r][c] = sum_d
+// grid (H, D / 64, ceil(R / 32)), 128 threads: 64 columns of one head for up
+// to 32 rows.  qt: [R][NS][HP][D] f16 planes (rows of padded heads h >= H are
+// never written: zeroed once at allocation).  out[r][c] = sum_d
 // q[r][h*64+d] Wk[h*64+d][c] as a 32 x 64 x 64 f16x2 product (A = q rows
 // split hi + lo from f32, B = the exact Wk values split hi + lo; the dropped
 // lo * lo term is < 2^-22 relative).  The 64 x 64 Wk block is dequantised
@@ -182,7 +132,7 @@ __global__ __launch_bounds__(128) void xattn_q_mfma_kernel(const float* __restri
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
       _Float16 hi, lo;
-      split_f16(v[i], hi, lo);
+      split_f16(v[i] * kWkScale, hi, lo);
       wth[(b * 32 + i) * LD + d] = hi;
       wtl[(b * 32 + i) * LD + d] = lo;
     }
@@ -193,7 +143,7 @@ __global__ __launch_bounds__(128) void xattn_q_mfma_kernel(const float* __restri
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       _Float16 x, y;
-      split_f16(xa[ks][j >> 2][j & 3], x, y);
+      wq4::split_act(xa[ks][j >> 2][j & 3], x, y);
       ah[ks][j] = x;
       al[ks][j] = y;
     }
@@ -215,7 +165,7 @@ __global__ __launch_bounds__(128) void xattn_q_mfma_kernel(const float* __restri
     const int r = r0 + (i & 3) + 8 * (i >> 2) + 4 * kh;
     if (r < R) {
       _Float16 x, y;
-      split_f16(acc[i] * kXqScale, x, y);
+      split_f16(acc[i] * kXqInv * kXqScale * kQtScale, x, y);
       qt[(((size_t)r * NS + 0) * HP + h) * D + c0 + c] = x;
       if (NS == 2) qt[(((size_t)r * NS + 1) * HP + h) * D + c0 + c] = y;
     }
@@ -231,11 +181,11 @@ __global__ __launch_bounds__(128) void xattn_q_mfma_kernel(const float* __restri
 // heads, k = the 16 frames read transposed from the same LDS image by
 // ds_read_b64_tr_b16; accumulators stay in registers).  Writes per (row,
 // split): Z [H][D] and (max, sum) [H].
-template <int D, int HT, int NS, int NW, int PF, int AUX = 0, int MODE = 0>
+template <int D, int HT, int NS, int NW, int PF>
 __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __restrict__ qt,
                                                              const _Float16* __restrict__ enc, int Tq, int T,
                                                              int H, int S, int CH, float* __restrict__ zpart,
-                                                             float* __restrict__ mlpart, int R, int xmap) {
+                                                             float* __restrict__ mlpart, int R) {
   constexpr int kThreads = 64 * NW;
   constexpr int CW = D / NW;      // columns per wave
   constexpr int KS = CW / 32;     // 32-column steps per wave (score k-steps = Z column tiles)
@@ -254,19 +204,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   __shared__ __attribute__((aligned(16))) _Float16 szero[8];
   __shared__ __attribute__((aligned(16))) _Float16 sq1[HT == 2 ? NS : 1][4][HT == 2 ? D + 16 : 8];
 
-  // xmap: 1-D grid of 8 * ceil(R / 8) * S workgroups dispatched round-robin
-  // over the 8 XCDs (L % 8); XCD x takes rows x, x + 8, ... with all their
-  // splits, so xattn_out (same map) reads the split partials from its own L2
-  int s, r;
-  if (xmap) {
-    const int L = blockIdx.x, x = L & 7, k = L >> 3;
-    s = k % S;
-    r = x + 8 * (k / S);
-    if (r >= R) return;  // whole workgroup, before any barrier
-  } else {
-    s = blockIdx.x;
-    r = blockIdx.y;
-  }
+  const int s = blockIdx.x, r = blockIdx.y;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int l16 = l & 15, lq = l >> 4, l32 = l & 31, lh = l >> 5;
   const _Float16* E = enc + (size_t)(r / Tq) * T * ROW;
@@ -335,7 +273,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     for (int i = 0; i < NLD; ++i) {
       int row, col;
       item(i, row, col);
-      buf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(((chi * kTc + row) * ROW + col) * 2), 0, AUX);
+      buf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(((chi * kTc + row) * ROW + col) * 2), 0, 0);
     }
   };
 
@@ -363,7 +301,6 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     }
   };
 
-  float sink = 0.0f;
   // scores of this wave's column slice: A = enc (m = frame, k = column) from
   // afrag(ks, plane), B = qt (k = column, n = head); partial sums to red
   auto scores = [&](auto&& afrag) {
@@ -411,17 +348,17 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
         const bool valid = h < H && t0 + t < te;
         sv = valid ? sv : -INFINITY;
         const float cm = wq4::max16(sv);  // DPP butterfly over the head's 16 frames
-        const float mn = fmaxf(M[e], cm);
+        const float mn = fmaxf(M[e], cm);  // scores (and M) carry the 2^10 operand scale
         float alpha = 1.0f, p = 0.0f;
         if (mn != -INFINITY) {
-          alpha = __builtin_amdgcn_exp2f(M[e] - mn);
-          p = valid ? __builtin_amdgcn_exp2f(sv - mn) : 0.0f;
+          alpha = __builtin_amdgcn_exp2f((M[e] - mn) * kSInv);
+          p = valid ? __builtin_amdgcn_exp2f((sv - mn) * kSInv) : 0.0f;
         }
         const float ps = wq4::sum16(p);
         L[e] = L[e] * alpha + ps;
         M[e] = mn;
         _Float16 phi, plo;
-        split_f16(p, phi, plo);
+        split_f16(p * kPScale, phi, plo);  // p * 2^15: the lo half stays a normal f16 (undone at the store)
         sp[0][h][t] = phi;
         if (NS == 2) sp[1][h][t] = plo;
         if (t == 0) salpha[h] = alpha;
@@ -468,11 +405,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   auto step = [&](u32x4v (&buf)[NLD], int chi) {
     const int t0 = ts + chi * kTc;
     write_se(buf);
-    if (MODE != 2 && chi + PF < nch) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
-    if constexpr (MODE == 1) {  // probe: the load / LDS-write skeleton alone (one LDS read keeps it live)
-      sink += (float)se[(tid * 9) % (kTc * RS)];
-      return;
-    }
+    if (chi + PF < nch) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
     scores([&](int ks, int p) {
       return *reinterpret_cast<const half8*>(&se[l16 * RS + p * D + c0 + ks * 32 + 8 * lq_sw]);
     });
@@ -493,7 +426,6 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     for (int chi = 0; chi < nch; ++chi) step(pre0, chi);
   }
 
-  if constexpr (MODE == 1) zacc[0][0] += sink * 1e-30f;
   // partials of this (row, split)
   const size_t base = (size_t)r * S + s;
 #pragma unroll
@@ -502,7 +434,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     if (idx < HT * 256 && (idx & 15) == 0) {
       const int h = (idx >> 8) * 16 + ((idx >> 4) & 15);
       if (h < H) {
-        mlpart[(base * H + h) * 2] = M[e];
+        mlpart[(base * H + h) * 2] = M[e] * kSInv;  // unscaled base-2 maximum (xattn_out's merge)
         mlpart[(base * H + h) * 2 + 1] = L[e];
       }
     }
@@ -512,7 +444,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     const int h = (j & 3) + 8 * (j >> 2) + 4 * lh;
     if (h < H) {
 #pragma unroll
-      for (int ct = 0; ct < KS; ++ct) zpart[(base * H + h) * D + c0 + ct * 32 + l32] = zacc[ct][j];
+      for (int ct = 0; ct < KS; ++ct) zpart[(base * H + h) * D + c0 + ct * 32 + l32] = zacc[ct][j] * kZInv;
     }
   }
 }
@@ -530,8 +462,7 @@ template <int NS, int WK, int RPW, int SM>
 __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict__ zpart,
                                                         const float* __restrict__ mlpart, int R, int H, int D, int S,
                                                         const uint8_t* __restrict__ wv,
-                                                        const float* __restrict__ bv, _Float16* __restrict__ tiled,
-                                                        int xmap) {
+                                                        const float* __restrict__ bv, _Float16* __restrict__ tiled) {
   constexpr int kStage = WK == kWtQ4 ? 64 * (kMaxD / 32) * 18 : 16;  // 46 KB of Q4 blocks
   __shared__ __attribute__((aligned(16))) uint8_t sw[kStage];
   // Zn of the RPW rows: f32 [column][row] (f16 weights, VALU projection) or
@@ -543,20 +474,7 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
   _Float16* zl = zh + RPW * ZLD;
   __shared__ __attribute__((aligned(16))) _Float16 zzero[8];
   __shared__ float red[16][64][RPW + 1];
-  // rows rbase + rstep * j; xmap (see xattn_main_kernel): 1-D grid, XCD x =
-  // L % 8 takes rows x + 8 (RPW g + j) of head h
-  int h, rbase, rstep;
-  if (xmap) {
-    const int L = blockIdx.x, x = L & 7, k = L >> 3;
-    h = k % H;
-    rbase = x + 8 * RPW * (k / H);
-    rstep = 8;
-    if (rbase >= R) return;  // no rows here (R < 8): whole workgroup, before any barrier
-  } else {
-    h = blockIdx.x;
-    rbase = blockIdx.y * RPW;
-    rstep = 1;
-  }
+  const int h = blockIdx.x, rbase = blockIdx.y * RPW, rstep = 1;
   const int tid = threadIdx.x;
   const int nkb = D / 32;
   // the value bias of this thread's final outputs, loaded up front
@@ -622,7 +540,7 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           _Float16 x, y;
-          split_f16(rok ? acc[e] / lsum : 0.0f, x, y);
+          split_f16(rok ? acc[e] / lsum * kZnScale : 0.0f, x, y);
           hi[e] = x;
           lo[e] = y;
         }
@@ -659,7 +577,7 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const uint16_t* blk = reinterpret_cast<const uint16_t*>(&sw[(size_t)(mt * 16 + n) * rowbytes + (size_t)kb * 18]);
-        const _Float16 d = __builtin_bit_cast(_Float16, blk[0]);
+        const _Float16 d = __builtin_bit_cast(_Float16, blk[0]) * (_Float16)kWvScale;  // exact: d < 16
         const half2v off = {(_Float16)1032.0f, (_Float16)1032.0f};
         const half2v dv = {d, d};
         half8 ah, al;
@@ -721,7 +639,7 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
     const int j = tid >> 6, d = tid & 63, r = rbase + rstep * j;
     float sacc = bias1;
 #pragma unroll
-    for (int g = 0; g < NPART; ++g) sacc += red[g][d][j];
+    for (int g = 0; g < NPART; ++g) sacc += red[g][d][j] * (WK == kWtQ4 ? kOutInv : 1.0f);  // exact rescale
     const float v1 = __shfl_down(sacc, 1, 64), v2 = __shfl_down(sacc, 2, 64), v3 = __shfl_down(sacc, 3, 64);
     if (r < R && (d & 3) == 0) atile_store4<NS>(tiled, r, h * 64 + d, kbp_of(D), sacc, v1, v2, v3);
   }
@@ -736,7 +654,7 @@ __global__ __launch_bounds__(256) void enc_planes_kernel(const float* __restrict
   const int64_t row = i / D;
   const int c = (int)(i - row * D);
   _Float16 hi, lo;
-  split_f16(x[i], hi, lo);
+  split_f16(x[i] * kEncScale, hi, lo);
   out[(row * NS) * D + c] = hi;
   if (NS == 2) out[(row * NS + 1) * D + c] = lo;
 }
@@ -751,7 +669,7 @@ __global__ __launch_bounds__(256) void untile_kernel(const _Float16* __restrict_
   const int r = i / K, k = i - r * K;
   float v = (float)t[wq4::atile_index(r, k, kbp_of(K), NS, 0)];
   if (NS == 2) v += (float)t[wq4::atile_index(r, k, kbp_of(K), NS, 1)];
-  out[i] = v;
+  out[i] = v * wq4::kActScaleInv;
 }
 
 // 8 waves (two per SIMD, 256 registers each: the Z accumulators of an
@@ -760,57 +678,19 @@ __global__ __launch_bounds__(256) void untile_kernel(const _Float16* __restrict_
 // fit the register file at Large-V3 f16x2.
 template <int D, int HT, int NS>
 void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T, int H, int S, int CH, float* z,
-                 float* ml, int R, int xmap, hipStream_t st) {
-  static const int variant = [] {  // probe knob: 1 = the load skeleton alone (wrong results)
-    const char* e = getenv("WA_XATTN_MAIN");
-    return e ? atoi(e) : 0;
-  }();
-  if constexpr ((D / 8) % 32 == 0) {
-    if (variant == 2) {  // probe (wrong results): compute on the first sub-chunk only, no further loads
-      hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1, 0, 2>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z,
-                         ml, R, xmap);
-      return;
-    }
-    if (variant == 1) {  // probe (wrong results): loads + LDS writes + barriers only
-      hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1, 0, 1>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z,
-                         ml, R, xmap);
-      return;
-    }
-    hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z, ml, R,
-                       xmap);
-  } else {
-    hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 4, 1>), g, dim3(256), 0, st, qt, enc, Tq, T, H, S, CH, z, ml, R,
-                       xmap);
-  }
+                 float* ml, int R, hipStream_t st) {
+  if constexpr ((D / 8) % 32 == 0)
+    hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z, ml, R);
+  else
+    hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 4, 1>), g, dim3(256), 0, st, qt, enc, Tq, T, H, S, CH, z, ml, R);
 }
 
-// rows of Zn per xattn_out workgroup (WA_XATTN_OUT_ROWS = 1, 2 or 4)
-int xattn_out_rows() {
-  static const int v = [] {
-    const char* e = getenv("WA_XATTN_OUT_ROWS");
-    const int r = e ? atoi(e) : 4;  // measured: 4 rows beat 1 or 2 (Wv stage shared by more rows)
-    return (r == 1 || r == 2) ? r : 4;
-  }();
-  return v;
-}
+constexpr int kOutRows = 4;  // rows of Zn per xattn_out workgroup (measured: 4 beat 1, 2 and 8)
 template <int NS, int WK>
-void launch_out(int rpw, dim3 go, const float* z, const float* ml, int R, int H, int D, int S, const uint8_t* wv,
-                const float* bv, _Float16* tiled, int xmap, hipStream_t st) {
-  // SM: unrolled split slots of the merge (8 for the default plan)
-#define WA_XOUT(RPW_, SM_)                                                                                   \
-  hipLaunchKernelGGL((xattn_out_kernel<NS, WK, RPW_, SM_>),                                                  \
-                     xmap ? dim3(8 * H * ((R + 8 * (RPW_)-1) / (8 * (RPW_)))) : go, dim3(512), 0, st, z, ml, R, H, D, \
-                     S, wv, bv, tiled, xmap)
-  if (S > 8) {
-    WA_XOUT(4, kMaxSplits);  // larger split counts (WA_XATTN_SPLITS): 4 rows per workgroup
-  } else if (rpw == 4) {
-    WA_XOUT(4, 8);
-  } else if (rpw == 2) {
-    WA_XOUT(2, 8);
-  } else {
-    WA_XOUT(1, 8);
-  }
-#undef WA_XOUT
+void launch_out(dim3 go, const float* z, const float* ml, int R, int H, int D, int S, const uint8_t* wv,
+                const float* bv, _Float16* tiled, hipStream_t st) {
+  hipLaunchKernelGGL((xattn_out_kernel<NS, WK, kOutRows, kXattnSplits>), go, dim3(512), 0, st, z, ml, R, H, D, S, wv,
+                     bv, tiled);
 }
 
 }  // namespace
@@ -821,9 +701,7 @@ void launch_out(int rpw, dim3 go, const float* z, const float* ml, int R, int H,
 XattnPlan xattn_plan(int R, int T) {
   (void)R;
   const int nchunk = (T + kTc - 1) / kTc;
-  int S = 8;
-  if (const char* e = getenv("WA_XATTN_SPLITS")) S = atoi(e);
-  S = std::max(1, std::min({S, nchunk, kMaxSplits}));
+  const int S = std::max(1, std::min(kXattnSplits, nchunk));
   XattnPlan p;
   p.ch = (nchunk + S - 1) / S;
   p.splits = (nchunk + p.ch - 1) / p.ch;
@@ -865,44 +743,21 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   float* ml = part + (size_t)R * p.splits * H * D;
   // qt = Wk^T q / 8
   const dim3 gq(H, D / 64, (R + 31) / 32);
-  static const bool q_mfma = [] {
-    const char* e = getenv("WA_XATTN_Q_MFMA");
-    return e ? atoi(e) != 0 : true;
-  }();
-  if (q_mfma) {
 #define WA_XQ(NS_, WK_) hipLaunchKernelGGL((xattn_q_mfma_kernel<NS_, WK_>), gq, dim3(128), 0, st, q, R, D, wk, HP, qt)
-    if (wtype == kWtQ4) {
-      if (ns == 2) WA_XQ(2, kWtQ4); else WA_XQ(1, kWtQ4);
-    } else {
-      if (ns == 2) WA_XQ(2, kWtF16); else WA_XQ(1, kWtF16);
-    }
-#undef WA_XQ
-  } else if (wtype == kWtQ4) {
-    if (ns == 2)
-      hipLaunchKernelGGL((xattn_q_kernel<2, kWtQ4>), gq, dim3(256), 0, st, q, R, D, wk, HP, qt);
-    else
-      hipLaunchKernelGGL((xattn_q_kernel<1, kWtQ4>), gq, dim3(256), 0, st, q, R, D, wk, HP, qt);
+  if (wtype == kWtQ4) {
+    if (ns == 2) WA_XQ(2, kWtQ4); else WA_XQ(1, kWtQ4);
   } else {
-    if (ns == 2)
-      hipLaunchKernelGGL((xattn_q_kernel<2, kWtF16>), gq, dim3(256), 0, st, q, R, D, wk, HP, qt);
-    else
-      hipLaunchKernelGGL((xattn_q_kernel<1, kWtF16>), gq, dim3(256), 0, st, q, R, D, wk, HP, qt);
+    if (ns == 2) WA_XQ(2, kWtF16); else WA_XQ(1, kWtF16);
   }
+#undef WA_XQ
   // stream the encoder output
-  // XCD-affine rows for xattn_main / xattn_out (WA_XATTN_XCD=1).  Off by
-  // default: measured 5 % slower per decode step with two 16-clip groups
-  // (the partials do not stay in the XCD's L2 across the kernel boundary).
-  static const int xmap = [] {
-    const char* e = getenv("WA_XATTN_XCD");
-    return e ? atoi(e) != 0 : 0;
-  }();
-  const dim3 gm = xmap ? dim3(8 * ((R + 7) / 8) * p.splits) : dim3(p.splits, R);
+  const dim3 gm(p.splits, R);
 #define WA_XMAIN(DD, HH)                                                          \
   if (D == DD && HT == HH) {                                                      \
     if (ns == 2)                                                                  \
-      launch_main<DD, HH, 2>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, R, xmap, st);   \
+      launch_main<DD, HH, 2>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, R, st); \
     else                                                                          \
-      launch_main<DD, HH, 1>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, R, xmap, st);   \
+      launch_main<DD, HH, 1>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, R, st); \
   } else
   WA_XMAIN(1280, 2)
   WA_XMAIN(1024, 1)
@@ -912,18 +767,17 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   return hipErrorInvalidValue;
 #undef WA_XMAIN
   // merge the splits and project with Wv into the output projection's operand
-  const int rpw = xattn_out_rows();
-  const dim3 go(H, (R + rpw - 1) / rpw);
+  const dim3 go(H, (R + kOutRows - 1) / kOutRows);
   if (wtype == kWtQ4) {
     if (ns == 2)
-      launch_out<2, kWtQ4>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, xmap, st);
+      launch_out<2, kWtQ4>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
     else
-      launch_out<1, kWtQ4>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, xmap, st);
+      launch_out<1, kWtQ4>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
   } else {
     if (ns == 2)
-      launch_out<2, kWtF16>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, xmap, st);
+      launch_out<2, kWtF16>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
     else
-      launch_out<1, kWtF16>(rpw, go, z, ml, R, H, D, p.splits, wv, bv, tiled, xmap, st);
+      launch_out<1, kWtF16>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
   }
   return hipGetLastError();
 }

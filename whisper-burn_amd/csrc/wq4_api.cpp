@@ -108,8 +108,9 @@ wq4_status decode_ws_get(int dev, void* stream, const wq4::DecodeWs** out) {
       return fail(WQ4_EINVAL,
                   "the first small-M GEMM on a stream must run outside graph capture (it allocates the split-K "
                   "workspace)");
-    wq4::DecodeWs ws{nullptr, nullptr};
+    wq4::DecodeWs ws{nullptr, nullptr, nullptr};
     hipError_t e = hipMalloc(&ws.part, (size_t)wq4::kDecodeWsFloats * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&ws.act_scale, 16);
     if (e == hipSuccess) e = hipMalloc(&ws.counters, (size_t)wq4::kDecodeMaxTiles * sizeof(int));
     if (e == hipSuccess)
       e = hipMemsetAsync(ws.counters, 0, (size_t)wq4::kDecodeMaxTiles * sizeof(int),
@@ -117,6 +118,7 @@ wq4_status decode_ws_get(int dev, void* stream, const wq4::DecodeWs** out) {
     if (e != hipSuccess) {
       if (ws.part) (void)hipFree(ws.part);
       if (ws.counters) (void)hipFree(ws.counters);
+      if (ws.act_scale) (void)hipFree(ws.act_scale);
       return fail(WQ4_ENOMEM, std::string("decode workspace: ") + hipGetErrorString(e));
     }
     it = g_decode_ws.emplace(std::make_pair(dev, stream), ws).first;
@@ -398,10 +400,17 @@ static wq4_status linear_impl(const wq4_tensor* w, const float* bias, const floa
   if (!dg.ok) return fail(WQ4_EHIP, "hipSetDevice failed");
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto* at = static_cast<_Float16*>(ws);
-  hipError_t e = wq4::launch_tile_activations(x, at, (int)rows, (int)k, (int)k, ns, st);
+  // the reference API takes any f32 input: the operand scale is chosen per
+  // call from max |x| (device-side, stream-ordered)
+  const wq4::DecodeWs* dws = nullptr;
+  s = decode_ws_get(w->device, st, &dws);
+  if (s != WQ4_OK) return s;
+  hipError_t e = wq4::launch_act_scale(x, (int)rows, (int)k, (int)k, dws->act_scale, st);
+  if (e == hipSuccess) e = wq4::launch_tile_activations(x, at, (int)rows, (int)k, (int)k, ns, st, dws->act_scale);
   if (e != hipSuccess) return hip_fail(e, "tile_activations launch");
   wq4::EpiArgs epi = make_epi(bias, (flags & WQ4_EPI_RESIDUAL) ? residual : nullptr, y, (int)w->g.n, (int)rows,
                               (int)w->g.n, (flags & WQ4_EPI_GELU) != 0);
+  epi.act_inv = dws->act_scale + 1;
   return gemm(w, at, rows, epi, wq4::kEpiF32, ns, st, use_decode(rows));
 }
 
@@ -460,10 +469,17 @@ static wq4_status ffn_impl(const wq4_tensor* fc1, const float* b1, const wq4_ten
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto* a1 = static_cast<_Float16*>(ws);
   auto* a2 = reinterpret_cast<_Float16*>(static_cast<uint8_t*>(ws) + n1);
-  hipError_t e = wq4::launch_tile_activations(x, a1, (int)rows, (int)fc1->g.k, (int)fc1->g.k, ns, st);
+  const wq4::DecodeWs* dws = nullptr;
+  s = decode_ws_get(fc1->device, st, &dws);
+  if (s != WQ4_OK) return s;
+  hipError_t e = wq4::launch_act_scale(x, (int)rows, (int)fc1->g.k, (int)fc1->g.k, dws->act_scale, st);
+  if (e == hipSuccess)
+    e = wq4::launch_tile_activations(x, a1, (int)rows, (int)fc1->g.k, (int)fc1->g.k, ns, st, dws->act_scale);
   if (e != hipSuccess) return hip_fail(e, "tile_activations launch");
-  // fc1 + bias + GELU, written straight into fc2's operand layout.
+  // fc1 + bias + GELU, written straight into fc2's operand layout (the fixed
+  // internal operand scale: |gelu(fc1 x)| < 4094).
   wq4::EpiArgs e1 = make_epi(b1, nullptr, nullptr, (int)fc1->g.n, (int)rows, (int)fc1->g.n, true);
+  e1.act_inv = dws->act_scale + 1;
   e1.out_tiled = a2;
   e1.nbp_next = (int)fc2->g.nbp;
   wq4_status s1 = gemm(fc1, a1, rows, e1, wq4::kEpiTiled, ns, st, use_decode(rows));

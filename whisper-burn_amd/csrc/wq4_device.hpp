@@ -89,6 +89,16 @@ __device__ __forceinline__ void split_f16(float x, _Float16& hi, _Float16& lo) {
   lo = (_Float16)(x - (float)hi);
 }
 
+// The MFMAs flush f16 subnormal inputs (measured on gfx950 with denormals
+// enabled in the kernel descriptor: scripts/attn_precision_probe.py), so the
+// lo half of a pair is lost once |lo| < 2^-14 -- for an unscaled N(0, 1)
+// operand that is most elements below 4.  Every split operand is therefore
+// scaled by a power of two that keeps lo normal over its range, and the
+// product's scale is undone in f32 (exact).  GEMM A operands (activations,
+// the A-tiled layout): x * 2^4, |x| < 4094; undone through the column scale.
+constexpr float kActScale = 16.0f, kActScaleInv = 1.0f / 16.0f;
+__device__ __forceinline__ void split_act(float x, _Float16& hi, _Float16& lo) { split_f16(x * kActScale, hi, lo); }
+
 // Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming
 // §5 T1): blocks L, L+8, L+16, ... (one XCD under round-robin dispatch) get
 // consecutive logical ids, so neighbouring tiles share that XCD's L2.

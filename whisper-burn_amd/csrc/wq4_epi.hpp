@@ -40,6 +40,11 @@ struct EpiArgs {
   const float* lnf_stats_in;
   const float* lnf_wg;
   int lnf_tiles;
+  // Inverse scale of the A operand (device scalar) when the operand was tiled
+  // with a per-call scale (wq4_matmul / linear / ffn entry points: wide
+  // activation range); nullptr = the fixed kActScale of every internal
+  // producer (wq4_device.hpp split_act).
+  const float* act_inv;
 };
 
 // Output element index.  Row-major by default; head-major (hm_t > 0) writes

@@ -14,7 +14,15 @@ hipError_t launch_layernorm(const float* x, const float* w, const float* b, int 
                             float* out, hipStream_t st);
 
 // f32 [M, ld] row-major -> A-tiled f16 split (ns = 1 or 2).
-hipError_t launch_tile_activations(const float* x, _Float16* at, int M, int K, int ld, int ns, hipStream_t st);
+// scale: device [2] = {s, 1/s} written by launch_act_scale (x is tiled as x * s),
+// or nullptr: the fixed kActScale.
+hipError_t launch_tile_activations(const float* x, _Float16* at, int M, int K, int ld, int ns, hipStream_t st,
+                                   const float* scale = nullptr);
+// Per-call activation scale for the f32 entry points: s = the power of two
+// min(2^4, 2^floor(log2(16384 / max|x|))) keeps every hi half finite (|x s| <
+// 2^15) and the lo halves of the largest values normal; out[0] = s,
+// out[1] = 1 / s.
+hipError_t launch_act_scale(const float* x, int M, int K, int ld, float* out, hipStream_t st);
 
 // Split-K workspace of the decode kernel, one per (device, stream): partial
 // tiles and per-n-tile arrival counters (zeroed once, re-armed by the kernel).
@@ -26,6 +34,7 @@ constexpr int kDecodeMaxMTiles = 4;                     // rows <= 128 (launches
 struct DecodeWs {
   float* part;
   int* counters;
+  float* act_scale;  // [2]: the f32 entry points' per-call activation scale (launch_act_scale)
 };
 struct DecodePlan {
   int per;    // kernel instance: max block pairs per wave

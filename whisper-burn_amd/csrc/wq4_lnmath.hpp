@@ -59,7 +59,7 @@ __device__ __forceinline__ void atile_store4(_Float16* t, int row, int k, int kb
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     _Float16 x, y;
-    split_f16(v[j], x, y);
+    split_act(v[j], x, y);
     hi[j] = x;
     lo[j] = y;
   }

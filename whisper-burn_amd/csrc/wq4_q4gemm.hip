@@ -40,7 +40,8 @@ namespace wq4 {
 template <int NS, bool ALIGNED>
 __global__ __launch_bounds__(256) void tile_activations_kernel(const float* __restrict__ x,
                                                                _Float16* __restrict__ at, int M, int K,
-                                                               int ld, int mtiles, int kbp) {
+                                                               int ld, int mtiles, int kbp,
+                                                               const float* __restrict__ scale) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t total = (int64_t)mtiles * kbp * 2 * 64;
   if (idx >= total) return;
@@ -71,11 +72,12 @@ __global__ __launch_bounds__(256) void tile_activations_kernel(const float* __re
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = 0.0f;
   }
+  const float s = scale ? scale[0] : kActScale;
   half8 hi, lo;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     _Float16 a, c;
-    split_f16(v[j], a, c);
+    split_f16(v[j] * s, a, c);
     hi[j] = a;
     lo[j] = c;
   }
@@ -109,10 +111,10 @@ __device__ __forceinline__ void store_tiled_slab(const float* stage, const EpiAr
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         _Float16 x, y;
-        split_f16(a[j], x, y);
+        split_act(a[j], x, y);
         hi[j] = x;
         lo[j] = y;
-        split_f16(c[j], x, y);
+        split_act(c[j], x, y);
         hi[4 + j] = x;
         lo[4 + j] = y;
       }
@@ -259,8 +261,9 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
   }
 
   float cs[TN];
+  const float ainv = e.act_inv ? *e.act_inv : kActScaleInv;  // A operand scale (exact power of two)
 #pragma unroll
-  for (int nt = 0; nt < TN; ++nt) cs[nt] = active ? colscale[(nt0 + nt) * 32 + r] : 1.0f;
+  for (int nt = 0; nt < TN; ++nt) cs[nt] = active ? colscale[(nt0 + nt) * 32 + r] * ainv : 1.0f;
 
   if constexpr (EPI == kEpiF32) {
     if (active) {
@@ -415,7 +418,8 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
   const int slice = blockIdx.x - nt * ks;
   const int bp0 = min(nbp, (slice * W + wave) * chunk);  // chunk <= PER (launcher)
   const int cnt = max(0, min(nbp, bp0 + chunk) - bp0);
-  const float cs = colscale[nt * 32 + r];
+  // weight row scale x A operand scale (exact powers of two)
+  const float cs = colscale[nt * 32 + r] * (e.act_inv ? *e.act_inv : kActScaleInv);
   // 8-wave plans: the epilogue operands of this lane's two outputs (rows
   // acc_row(2 wave + q, h), column nt * 32 + r) are loaded up front so they
   // are not a memory round trip after the MFMAs (bias, residual: never
@@ -534,8 +538,8 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
                 _Float16 h0, l0, h1, l1;
-                split_f16(ln_apply(x0[j], mean, den, g0[j], b0[j]), h0, l0);
-                split_f16(ln_apply(x1[j], mean, den, g1[j], b1[j]), h1, l1);
+                split_act(ln_apply(x0[j], mean, den, g0[j], b0[j]), h0, l0);
+                split_act(ln_apply(x1[j], mean, den, g1[j], b1[j]), h1, l1);
                 hi[j] = h0;
                 lo[j] = l0;
                 hi[4 + j] = h1;
@@ -898,7 +902,34 @@ DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal) {
   return p;
 }
 
-hipError_t launch_tile_activations(const float* x, _Float16* at, int M, int K, int ld, int ns, hipStream_t st) {
+__global__ __launch_bounds__(1024) void act_scale_kernel(const float* __restrict__ x, int M, int K, int ld,
+                                                         float* __restrict__ out) {
+  __shared__ float red[16];
+  float mx = 0.0f;
+  for (int64_t i = threadIdx.x; i < (int64_t)M * K; i += 1024) {
+    const int64_t m = i / K;
+    mx = fmaxf(mx, fabsf(x[m * ld + (i - m * K)]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 16; ++w) mx = fmaxf(mx, red[w]);
+    int e = 4;  // the internal producers' 2^4, unless the range needs less
+    if (mx > 0.0f && mx < INFINITY) e = min(4, (int)floorf(log2f(16384.0f / mx)));
+    out[0] = ldexpf(1.0f, e);
+    out[1] = ldexpf(1.0f, -e);
+  }
+}
+
+hipError_t launch_act_scale(const float* x, int M, int K, int ld, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(act_scale_kernel, dim3(1), dim3(1024), 0, st, x, M, K, ld, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_tile_activations(const float* x, _Float16* at, int M, int K, int ld, int ns, hipStream_t st,
+                                   const float* scale) {
   const int mtiles = (int)(round_up(M < 1 ? 1 : M, kMPad) / kMTile);
   const int kbp = (int)(((K / kBlock) + 1) / 2) * 2;
   const int64_t total = (int64_t)mtiles * kbp * 2 * 64;
@@ -906,7 +937,7 @@ hipError_t launch_tile_activations(const float* x, _Float16* at, int M, int K, i
   const bool aligned = (ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) & 15u) == 0);
 #define WQ4_TILE(NS_, AL_)                                                                                   \
   hipLaunchKernelGGL((tile_activations_kernel<NS_, AL_>), dim3(grid), dim3(256), 0, st, x, at, M, K, ld, mtiles, \
-                     kbp)
+                     kbp, scale)
   if (ns == 2) {
     if (aligned) WQ4_TILE(2, true); else WQ4_TILE(2, false);
   } else {

@@ -66,7 +66,12 @@ def lib() -> ctypes.CDLL:
         L.wa_log_mel.argtypes = [c_int, vp, c_int, c_i64, c_i64, c_int, vp, vp]
         L.wa_mel_filterbank.argtypes = [c_int, f32p, f32p]
         L.wa_xattn_check.argtypes = [c_int, vp, vp, vp, vp, c_int, vp, c_int, c_int, c_int, c_int, c_int, vp]
-        for n in ("wa_xattn_check", "wa_log_mel", "wa_mel_filterbank", "wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
+        L.wa_transcribe_trace.argtypes = [vp, vp, c_int, c_int, c_int, c_int, i32p, i32p, vp, c_int, vp, vp]
+        L.wa_encoder_attention_check.argtypes = [c_int, vp, c_int, c_int, c_int, c_int, vp]
+        L.wa_self_attention_check.argtypes = [c_int, vp, vp, vp, c_int, c_int, c_int, c_int, c_int, c_int, vp]
+        L.wa_logits_argmax_check.argtypes = [c_int, vp, vp, c_int, c_int, c_int, c_int, c_int, vp, vp]
+        for n in ("wa_xattn_check", "wa_transcribe_trace", "wa_encoder_attention_check", "wa_self_attention_check",
+                  "wa_logits_argmax_check", "wa_log_mel", "wa_mel_filterbank", "wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
                   "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read", "wa_probe_kernels",
                   "wa_model_create_from_gguf", "wa_model_create_synthetic_ex", "wa_gguf_open", "wa_gguf_tensor_info", "wa_gguf_tensor_data"):
             getattr(L, n).restype = c_int
@@ -138,6 +143,51 @@ def xattn_check(q, wk_raw, wv_raw, bv, enc, Tq: int, H: int, weight_type: int = 
     check(lib().wa_xattn_check(dev, ptr(q), ptr(wk_raw), ptr(wv_raw), ptr(bv), weight_type, ptr(enc), B, Tq, T, H,
                                precision, ptr(out)))
     return out
+
+
+def _dev(t) -> int:
+    return t.device.index if t.device.index is not None else 0
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def encoder_attention_check(qkv, T: int, H: int, precision: int = wq4.PREC_F16X2):
+    """Encoder self-attention through the product kernel (wa_encoder_attention_check):
+    qkv cuda f32 [B*T, 3*64H] -> [B*T, 64H]."""
+    torch = _torch()
+    qkv = qkv.contiguous()
+    B = qkv.shape[0] // T
+    out = torch.empty((B * T, 64 * H), device=qkv.device, dtype=torch.float32)
+    check(lib().wa_encoder_attention_check(_dev(qkv), _ptr(qkv), B, T, H, precision, _ptr(out)))
+    return out
+
+
+def self_attention_check(qkv, cache_k, cache_v, Tq: int, H: int, kv_len: int, precision: int = wq4.PREC_F16X2):
+    """Decoder self-attention through the product kernel (wa_self_attention_check):
+    qkv cuda f32 [B*Tq, 3*64H]; caches [B, H, ctx, 64] (updated in place:
+    the new keys / values appended at kv_len) -> [B*Tq, 64H]."""
+    torch = _torch()
+    B, _, ctx, _ = cache_k.shape
+    out = torch.empty((B * Tq, 64 * H), device=qkv.device, dtype=torch.float32)
+    check(lib().wa_self_attention_check(_dev(qkv), _ptr(qkv.contiguous()), _ptr(cache_k), _ptr(cache_v), B, Tq, H,
+                                        ctx, kv_len, precision, _ptr(out)))
+    return out
+
+
+def logits_argmax_check(hid, emb, step: int, precision: int = wq4.PREC_F16X2, want_logits: bool = True):
+    """The decode step's fused logits + greedy pick (wa_logits_argmax_check):
+    hid cuda f32 [B, D], emb cuda f32 [V, D] -> (tokens int32 [B], logits
+    [B, V] as the pick saw them, or None)."""
+    torch = _torch()
+    B, D = hid.shape
+    V = emb.shape[0]
+    tok = torch.empty(B, device=hid.device, dtype=torch.int32)
+    lg = torch.empty((B, V), device=hid.device, dtype=torch.float32) if want_logits else None
+    check(lib().wa_logits_argmax_check(_dev(hid), _ptr(hid.contiguous()), _ptr(emb.contiguous()), B, D, V, step,
+                                       precision, _ptr(tok), _ptr(lg) if lg is not None else None))
+    return tok, lg
 
 
 class GgufReader:
@@ -235,6 +285,27 @@ class WhisperModel:
                                   -1 if lang_token is None else int(lang_token), max_tokens, 1 if eot_stop else 0,
                                   toks.ctypes.data_as(i32p), nt.ctypes.data_as(i32p), self._stream()))
         return [toks[b, : nt[b]].tolist() for b in range(B)]
+
+    def transcribe_trace(self, mel, trace_ids: np.ndarray, lang_token: Optional[int] = 50259,
+                         max_tokens: int = 224, eot_stop: bool = False):
+        """transcribe + the decode-step logit trace (wa_transcribe_trace):
+        trace_ids int32 [B, max_tokens + 1, K] -> (tokens, logits [B,
+        max_tokens + 1, K] float32; slot 0 and slots past a clip's last step
+        are NaN)."""
+        torch = _torch()
+        mel = mel.contiguous()
+        B = mel.shape[0]
+        K = trace_ids.shape[-1]
+        assert trace_ids.shape == (B, max_tokens + 1, K)
+        ids = torch.from_numpy(np.ascontiguousarray(trace_ids, np.int32)).to(mel.device)
+        out = torch.full((B, max_tokens + 1, K), float("nan"), device=mel.device, dtype=torch.float32)
+        toks = np.zeros((B, max_tokens), np.int32)
+        nt = np.zeros(B, np.int32)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        check(lib().wa_transcribe_trace(self._h, _ptr(mel), B, -1 if lang_token is None else int(lang_token),
+                                        max_tokens, 1 if eot_stop else 0, toks.ctypes.data_as(i32p),
+                                        nt.ctypes.data_as(i32p), _ptr(ids), K, _ptr(out), self._stream()))
+        return [toks[b, : nt[b]].tolist() for b in range(B)], out.cpu().numpy()
 
     def transcribe_audio(self, audio, lang_token: Optional[int] = 50259, max_tokens: int = 224,
                          eot_stop: bool = True, n_samples: Optional[int] = None):
