@@ -155,7 +155,8 @@ wq4_status wq4_linear_forward_tiled_out(const wq4_tensor* w, const float* bias_d
                                         wq4_precision prec, void* stream);
 
 /* Extended operand-layout GEMM used by the model runtime: explicit kernel
- * (0 = automatic by rows, 1 = MFMA tile "prefill", 2 = K-split "decode"),
+ * (0 = automatic by rows, 1 = MFMA tile "prefill", 2 = K-split "decode",
+ * 3 = the decode-step kernel: rows <= 32, K % 128 == 0, N % 16 == 0),
  * output f32 row-major y_dev, or, with WQ4_EPI_TILED_OUT, the A-tiled
  * operand at_out_dev of a following GEMM (K' = N; N % 32 == 0).           */
 #define WQ4_EPI_TILED_OUT 4u
@@ -178,8 +179,8 @@ wq4_status wq4_gemm_ln_tiled(const wq4_tensor* w, const float* bias_dev, const f
                              void* at_out_dev, int64_t rows, unsigned flags, wq4_precision prec, int kernel,
                              void* stream);
 
-/* LayerNorm folded into the decoder GEMMs around it (decode-sized rows,
- * the 8-wave decode plans; replaces the wq4_layernorm launch between a
+/* LayerNorm folded into the decoder GEMMs around it (the decode-step
+ * kernel: rows <= 32, K % 128 == 0, N % 16 == 0; replaces the wq4_layernorm launch between a
  * residual GEMM and the GEMM that reads LayerNorm of its output -- the
  * attn_ln / cross_attn_ln / mlp_ln -> Q4Linear pairs of decoder.rs:77-112).
  * LN(x) = (x - mean) / sqrt(var + 1e-5) * gamma + beta (layers.rs:12-32), so
@@ -187,9 +188,9 @@ wq4_status wq4_gemm_ln_tiled(const wq4_tensor* w, const float* bias_dev, const f
  *                    + (W beta + bias).
  * Producer (set gamma_dev, at_out_dev, stats_out_dev): a residual GEMM
  * (WQ4_EPI_RESIDUAL, f32 output x) also writes the A-tiled operand of
- * x * gamma (wq4_atiled_bytes(rows, N, prec)) and, per (row, 32-column
+ * x * gamma (wq4_atiled_bytes(rows, N, prec)) and, per (row, 16-column
  * tile), the tile mean and sum of squared deviations (stats_out_dev,
- * rows * N/32 * 2 floats).  Consumer (set stats_in_dev, wg_dev): at_dev is
+ * rows * N/16 * 2 floats).  Consumer (set stats_in_dev, wg_dev): at_dev is
  * that operand; the row statistics are merged (Chan et al., fixed order)
  * and the correction applied before bias / GELU / tiled output; bias_dev is
  * W beta + bias and wg_dev W gamma (wq4_ln_fold_vectors).  A launch may be
@@ -198,8 +199,8 @@ wq4_status wq4_gemm_ln_tiled(const wq4_tensor* w, const float* bias_dev, const f
 typedef struct wq4_ln_fold {
   const float* gamma_dev;     /* producer: gamma of the LayerNorm that follows */
   void* at_out_dev;           /* producer: A-tiled x * gamma */
-  float* stats_out_dev;       /* producer: [rows][N/32][2] */
-  const float* stats_in_dev;  /* consumer: the producer's statistics (K/32 tiles) */
+  float* stats_out_dev;       /* producer: [rows][N/16][2] */
+  const float* stats_in_dev;  /* consumer: the producer's statistics (K/16 tiles) */
   const float* wg_dev;        /* consumer: W gamma [N] */
 } wq4_ln_fold;
 wq4_status wq4_gemm_tiled_lnfold(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
@@ -211,7 +212,7 @@ wq4_status wq4_gemm_tiled_lnfold(const wq4_tensor* w, const float* bias_dev, con
 wq4_status wq4_ln_fold_vectors(const wq4_tensor* w, const float* gamma, const float* beta, const float* bias,
                                float* wg_out, float* bias_out);
 /* Whether wq4_gemm_tiled_lnfold supports w at this row count (a consumer
- * also needs K % 32 == 0 and K <= 2048). */
+ * also needs K <= 1280). */
 int wq4_lnfold_supported(const wq4_tensor* w, int64_t rows);
 
 /* Allocate (once) the per-(device, stream) split-K workspace that small-M
@@ -246,8 +247,9 @@ wq4_status wq4_quantize_q4_0(const float* x, int64_t n, uint8_t* out);
 
 /* ---- kernel selection (exposed for tests and the bench) -------------- */
 /* 0 = automatic (by rows), 1 = force the MFMA tile kernel ("prefill"),
- * 2 = force the K-split streaming kernel ("decode").  Both compute each
- * output row with an M-independent instruction sequence. */
+ * 2 = force the K-split streaming kernel ("decode"), 3 = force the
+ * decode-step kernel (rows <= 32).  Each computes every output row with an
+ * M-independent instruction sequence. */
 wq4_status wq4_set_kernel_policy(int policy);
 
 /* ---- host-only diagnostics (no GPU needed) ---------------------------- */

@@ -20,7 +20,7 @@ for r in rows:
     byq[r.get("Queue_Id", "0")].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
 dur = collections.defaultdict(list)
 gap = collections.defaultdict(list)
-decode = re.compile(r"xattn|dec_self|q4_gemm_decode|logits_argmax|embed_fold|bookkeep")
+decode = re.compile(r"xattn|dec_self|q4_gemm_decode|skinny_gemm|logits_argmax|embed_fold|bookkeep")
 for q, ks in byq.items():
     ks.sort()
     for i in range(1, len(ks)):

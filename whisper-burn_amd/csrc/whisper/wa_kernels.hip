@@ -630,17 +630,18 @@ __global__ __launch_bounds__(256) void embed_fold_kernel(const int* __restrict__
       *reinterpret_cast<floatx4*>(x + (size_t)row * D + c) = v;
       atile_store4<NS>(at, row, c, kbp, v[0] * g[0], v[1] * g[1], v[2] * g[2], v[3] * g[3]);
     }
+    // statistics per 16-column tile (the decode-step GEMM's LayerNorm fold)
     float sum = (v[0] + v[1]) + (v[2] + v[3]);
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) sum += __shfl_xor(sum, o, 64);
-    const float mean = sum * (1.0f / 32.0f);
+    for (int o = 1; o < 4; o <<= 1) sum += __shfl_xor(sum, o, 64);
+    const float mean = sum * (1.0f / 16.0f);
     float m2 = 0.0f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) m2 += (v[j] - mean) * (v[j] - mean);
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) m2 += __shfl_xor(m2, o, 64);
-    if (in && (threadIdx.x & 7) == 0) {
-      float* st = stats + ((size_t)row * (D / 32) + c / 32) * 2;
+    for (int o = 1; o < 4; o <<= 1) m2 += __shfl_xor(m2, o, 64);
+    if (in && (threadIdx.x & 3) == 0) {
+      float* st = stats + ((size_t)row * (D / 16) + c / 16) * 2;
       st[0] = mean;
       st[1] = m2;
     }

@@ -638,7 +638,7 @@ wq4_status alloc_activations(wa_model* m) {
     g.xattn_part = f32((int64_t)xpart);
     g.xqt = d.alloc<_Float16>((size_t)rdec * m->ns * HP * Dt);
     g.atd_ln = tiled(rdec, Dt);
-    g.ln_stats = f32(rdec * (Dt / 32) * 2);
+    g.ln_stats = f32(rdec * (Dt / 16) * 2);  // per 16-column tile (the decode-step GEMM)
     g.lg_val = f32((int64_t)32 * wa::logits_argmax_groups(c.n_vocab));
     g.lg_idx = d.alloc<int>((size_t)32 * wa::logits_argmax_groups(c.n_vocab));
     g.lg_ctr = d.alloc<int>(1);

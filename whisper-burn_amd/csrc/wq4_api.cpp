@@ -34,6 +34,8 @@ struct wq4_tensor {
   uint8_t* raw = nullptr;    // device, raw GGUF bytes (flat tensors only)
   size_t raw_bytes = 0;
   int wtype = 0;             // wq4::kWeightsQ4, or kWeightsF16 (nib = f16 fragments, sc unused, cs = 1)
+  uint32_t* q16 = nullptr;   // device, the decode-step kernel's layout (wq4_skinny.hip): Q4 nibbles or f16s
+  uint16_t* d16 = nullptr;   // device, its f16 block scales (Q4 only)
 };
 
 namespace {
@@ -163,8 +165,32 @@ wq4_status check_gemm_tensor(const wq4_tensor* w) {
   return WQ4_OK;
 }
 
+bool skinny_ok(const wq4_tensor* w, int64_t rows) {
+  return w && w->q16 && wq4::skinny_supported(w->g, (int)rows);
+}
+
+// kernel 0 = by row count (<= 32 and a skinny layout: the decode-step kernel;
+// <= 128: the 8-wave decode kernel; else the prefill tile kernel), 1 =
+// prefill, 2 = decode, 3 = decode-step (skinny) kernel.
+int pick_kernel(const wq4_tensor* w, int64_t rows, int kernel) {
+  if (kernel != 0) return kernel;
+  const int pol = g_policy.load();
+  if (pol != 0) return pol == 3 && !skinny_ok(w, rows) ? 2 : pol;
+  if (skinny_ok(w, rows)) return 3;
+  return use_decode(rows) ? 2 : 1;
+}
+
 wq4_status gemm(const wq4_tensor* w, const _Float16* at, int64_t rows, const wq4::EpiArgs& e, int mode, int ns,
-                hipStream_t st, bool dec) {
+                hipStream_t st, bool dec, bool skinny = false) {
+  if (skinny) {
+    if (!skinny_ok(w, rows)) return fail(WQ4_ESHAPE, "the decode-step kernel needs rows <= 32, K % 128 == 0, N % 16 == 0");
+    const wq4::DecodeWs* ws = nullptr;
+    wq4_status s = decode_ws_get(w->device, st, &ws);
+    if (s != WQ4_OK) return s;
+    hipError_t he = wq4::launch_skinny_gemm(w->g, w->q16, w->d16, at, (int)rows, e, mode, ns, w->wtype, ws, st);
+    if (he != hipSuccess) return hip_fail(he, "skinny gemm launch");
+    return WQ4_OK;
+  }
   const wq4::DecodeWs* ws = nullptr;
   if (dec) {
     wq4_status s = decode_ws_get(w->device, st, &ws);
@@ -202,7 +228,7 @@ wq4_status wq4_set_precision(wq4_precision prec) {
 wq4_precision wq4_get_precision(void) { return static_cast<wq4_precision>(g_prec.load()); }
 
 wq4_status wq4_set_kernel_policy(int policy) {
-  if (policy < 0 || policy > 2) return fail(WQ4_EINVAL, "policy must be 0, 1 or 2");
+  if (policy < 0 || policy > 3) return fail(WQ4_EINVAL, "policy must be 0, 1, 2 or 3");
   g_policy.store(policy);
   return WQ4_OK;
 }
@@ -249,6 +275,15 @@ wq4_status wq4_tensor_create(int device, const uint8_t* raw, size_t nbytes, int6
     if (e == hipSuccess) e = hipMemcpy(t->nib, nib.data(), nib.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(t->sc, sc.data(), t->g.sc_bytes(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(t->cs, cs.data(), t->g.colscale_bytes(), hipMemcpyHostToDevice);
+    if (e == hipSuccess && k % 128 == 0 && n % 16 == 0) {  // the decode-step kernel's layout
+      std::vector<uint32_t> q16(wq4::skinny_q_bytes(t->g) / 4);
+      std::vector<uint16_t> d16(wq4::skinny_d_bytes(t->g) / 2);
+      wq4::repack_q4_skinny(raw, t->g, q16.data(), d16.data());
+      e = hipMalloc(&t->q16, wq4::skinny_q_bytes(t->g));
+      if (e == hipSuccess) e = hipMalloc(&t->d16, wq4::skinny_d_bytes(t->g));
+      if (e == hipSuccess) e = hipMemcpy(t->q16, q16.data(), wq4::skinny_q_bytes(t->g), hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMemcpy(t->d16, d16.data(), wq4::skinny_d_bytes(t->g), hipMemcpyHostToDevice);
+    }
   }
   if (e != hipSuccess) {
     wq4_tensor_destroy(t);
@@ -265,6 +300,8 @@ void wq4_tensor_destroy(wq4_tensor* t) {
   if (t->sc) (void)hipFree(t->sc);
   if (t->cs) (void)hipFree(t->cs);
   if (t->raw) (void)hipFree(t->raw);
+  if (t->q16) (void)hipFree(t->q16);
+  if (t->d16) (void)hipFree(t->d16);
   delete t;
 }
 
@@ -279,8 +316,10 @@ int64_t wq4_tensor_num_blocks(const wq4_tensor* t) { return t ? t->g.n * t->g.k 
 int wq4_tensor_device(const wq4_tensor* t) { return t ? t->device : -1; }
 size_t wq4_tensor_device_bytes(const wq4_tensor* t) {
   if (!t) return 0;
-  if (t->wtype == wq4::kWeightsF16) return t->g.f16_frag_bytes() + t->g.colscale_bytes();
-  return t->flat ? t->raw_bytes : t->g.nib_bytes() + t->g.sc_bytes() + t->g.colscale_bytes();
+  const size_t sk = !t->q16 ? 0 : t->wtype == wq4::kWeightsF16 ? wq4::skinny_f16_bytes(t->g)
+                                                                : wq4::skinny_q_bytes(t->g) + wq4::skinny_d_bytes(t->g);
+  if (t->wtype == wq4::kWeightsF16) return t->g.f16_frag_bytes() + t->g.colscale_bytes() + sk;
+  return t->flat ? t->raw_bytes : t->g.nib_bytes() + t->g.sc_bytes() + t->g.colscale_bytes() + sk;
 }
 
 wq4_status wq4_tensor_create_f16(int device, const uint16_t* w, int64_t n, int64_t k, wq4_tensor** out) {
@@ -304,6 +343,12 @@ wq4_status wq4_tensor_create_f16(int device, const uint16_t* w, int64_t n, int64
   if (e == hipSuccess) e = hipMalloc(&t->cs, t->g.colscale_bytes());
   if (e == hipSuccess) e = hipMemcpy(t->nib, frag.data(), t->g.f16_frag_bytes(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(t->cs, ones.data(), t->g.colscale_bytes(), hipMemcpyHostToDevice);
+  if (e == hipSuccess && k % 128 == 0 && n % 16 == 0) {  // the decode-step kernel's layout
+    std::vector<uint16_t> f16s(wq4::skinny_f16_bytes(t->g) / 2);
+    wq4::repack_f16_skinny(w, t->g, f16s.data());
+    e = hipMalloc(&t->q16, wq4::skinny_f16_bytes(t->g));
+    if (e == hipSuccess) e = hipMemcpy(t->q16, f16s.data(), wq4::skinny_f16_bytes(t->g), hipMemcpyHostToDevice);
+  }
   if (e != hipSuccess) {
     wq4_tensor_destroy(t);
     return hip_fail(e, "F16 weight upload");
@@ -411,7 +456,8 @@ static wq4_status linear_impl(const wq4_tensor* w, const float* bias, const floa
   wq4::EpiArgs epi = make_epi(bias, (flags & WQ4_EPI_RESIDUAL) ? residual : nullptr, y, (int)w->g.n, (int)rows,
                               (int)w->g.n, (flags & WQ4_EPI_GELU) != 0);
   epi.act_inv = dws->act_scale + 1;
-  return gemm(w, at, rows, epi, wq4::kEpiF32, ns, st, use_decode(rows));
+  const int kk = pick_kernel(w, rows, 0);
+  return gemm(w, at, rows, epi, wq4::kEpiF32, ns, st, kk == 2, kk == 3);
 }
 
 wq4_status wq4_linear_forward_ws(const wq4_tensor* w, const float* bias_dev, const float* x_dev,
@@ -482,11 +528,12 @@ static wq4_status ffn_impl(const wq4_tensor* fc1, const float* b1, const wq4_ten
   e1.act_inv = dws->act_scale + 1;
   e1.out_tiled = a2;
   e1.nbp_next = (int)fc2->g.nbp;
-  wq4_status s1 = gemm(fc1, a1, rows, e1, wq4::kEpiTiled, ns, st, use_decode(rows));
+  const int k1 = pick_kernel(fc1, rows, 0), k2 = pick_kernel(fc2, rows, 0);
+  wq4_status s1 = gemm(fc1, a1, rows, e1, wq4::kEpiTiled, ns, st, k1 == 2, k1 == 3);
   if (s1 != WQ4_OK) return s1;
   wq4::EpiArgs e2 = make_epi(b2, (flags & WQ4_EPI_RESIDUAL) ? residual : nullptr, y, (int)fc2->g.n, (int)rows,
                              (int)fc2->g.n, (flags & WQ4_EPI_GELU) != 0);
-  return gemm(fc2, a2, rows, e2, wq4::kEpiF32, ns, st, use_decode(rows));
+  return gemm(fc2, a2, rows, e2, wq4::kEpiF32, ns, st, k2 == 2, k2 == 3);
 }
 
 wq4_status wq4_ffn_forward_ws(const wq4_tensor* fc1, const float* b1_dev, const wq4_tensor* fc2,
@@ -551,7 +598,7 @@ wq4_status wq4_linear_forward_tiled(const wq4_tensor* w, const float* bias_dev, 
   wq4::EpiArgs epi = make_epi(bias_dev, (flags & WQ4_EPI_RESIDUAL) ? residual_dev : nullptr, y_dev, (int)w->g.n,
                               (int)rows, (int)w->g.n, (flags & WQ4_EPI_GELU) != 0);
   return gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, wq4::kEpiF32, ns_of(prec),
-              static_cast<hipStream_t>(stream), use_decode(rows));
+              static_cast<hipStream_t>(stream), pick_kernel(w, rows, 0) == 2, pick_kernel(w, rows, 0) == 3);
 }
 
 wq4_status wq4_linear_forward_tiled_out(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
@@ -574,7 +621,7 @@ wq4_status wq4_linear_forward_tiled_out(const wq4_tensor* w, const float* bias_d
   epi.out_tiled = static_cast<_Float16*>(at_out_dev);
   epi.nbp_next = (int)((w->g.n / 32 + 1) / 2);
   return gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, wq4::kEpiTiled, ns_of(prec),
-              static_cast<hipStream_t>(stream), use_decode(rows));
+              static_cast<hipStream_t>(stream), pick_kernel(w, rows, 0) == 2, pick_kernel(w, rows, 0) == 3);
 }
 
 wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void* at_dev, const float* residual_dev,
@@ -584,7 +631,7 @@ wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void
   if (s != WQ4_OK) return s;
   s = check_prec(prec);
   if (s != WQ4_OK) return s;
-  if (kernel < 0 || kernel > 2) return fail(WQ4_EINVAL, "kernel must be 0, 1 or 2");
+  if (kernel < 0 || kernel > 3) return fail(WQ4_EINVAL, "kernel must be 0, 1, 2 or 3");
   if (rows < 0 || rows > (1 << 24)) return fail(WQ4_ESHAPE, "bad row count");
   if (rows == 0) return WQ4_OK;
   const bool tiled_out = (flags & WQ4_EPI_TILED_OUT) != 0;
@@ -599,9 +646,9 @@ wq4_status wq4_gemm_tiled(const wq4_tensor* w, const float* bias_dev, const void
     epi.out_tiled = static_cast<_Float16*>(at_out_dev);
     epi.nbp_next = (int)((w->g.n / 32 + 1) / 2);
   }
-  const bool dec = kernel == 0 ? use_decode(rows) : kernel == 2;
+  const int kk = pick_kernel(w, rows, kernel);
   return gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, tiled_out ? wq4::kEpiTiled : wq4::kEpiF32,
-              ns_of(prec), static_cast<hipStream_t>(stream), dec);
+              ns_of(prec), static_cast<hipStream_t>(stream), kk == 2, kk == 3);
 }
 
 wq4_status wq4_gemm_ln_tiled(const wq4_tensor* w, const float* bias_dev, const float* x_dev, const float* ln_w_dev,
@@ -649,8 +696,8 @@ wq4_status wq4_gemm_ln_tiled(const wq4_tensor* w, const float* bias_dev, const f
 }
 
 int wq4_lnfold_supported(const wq4_tensor* w, int64_t rows) {
-  if (!w || w->flat || rows < 1 || rows > 32 * wq4::kDecodeMaxMTiles) return 0;
-  return wq4::decode_ln_supported(w->g, (int)rows) ? 1 : 0;
+  if (!w || w->flat || rows < 1) return 0;
+  return skinny_ok(w, rows) ? 1 : 0;  // the decode-step kernel's 16-column tile statistics
 }
 
 wq4_status wq4_gemm_tiled_lnfold(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
@@ -662,16 +709,17 @@ wq4_status wq4_gemm_tiled_lnfold(const wq4_tensor* w, const float* bias_dev, con
   if (s != WQ4_OK) return s;
   if (!fold) return fail(WQ4_EINVAL, "fold is null");
   if (rows == 0) return WQ4_OK;
-  if (!wq4_lnfold_supported(w, rows)) return fail(WQ4_ESHAPE, "LayerNorm fold needs a decode-sized 8-wave plan");
+  if (!wq4_lnfold_supported(w, rows))
+    return fail(WQ4_ESHAPE, "LayerNorm fold needs the decode-step kernel (rows <= 32, K % 128 == 0, N % 16 == 0)");
   const bool tiled_out = (flags & WQ4_EPI_TILED_OUT) != 0;
   const bool producer = fold->at_out_dev != nullptr, consumer = fold->stats_in_dev != nullptr;
   if (!at_dev || (tiled_out ? !at_out_dev : !y_dev)) return fail(WQ4_EINVAL, "null argument");
   if ((flags & WQ4_EPI_RESIDUAL) && (!residual_dev || tiled_out))
     return fail(WQ4_EINVAL, "WQ4_EPI_RESIDUAL needs a residual and an f32 output");
-  if (producer && (!fold->gamma_dev || !fold->stats_out_dev || tiled_out || w->g.n % 32 != 0 || w->g.n > 2048))
+  if (producer && (!fold->gamma_dev || !fold->stats_out_dev || tiled_out || w->g.n % 32 != 0))
     return fail(WQ4_EINVAL, "LayerNorm-fold producer needs gamma, statistics, an f32 output and N % 32 == 0");
-  if (consumer && (!fold->wg_dev || w->g.k % 32 != 0 || w->g.k / 32 > 64))
-    return fail(WQ4_EINVAL, "LayerNorm-fold consumer needs W gamma and K % 32 == 0, K <= 2048");
+  if (consumer && (!fold->wg_dev || w->g.k / 16 > wq4::kSkinnyMaxLnTiles))
+    return fail(WQ4_EINVAL, "LayerNorm-fold consumer needs W gamma and K <= 1280");
   if (tiled_out && w->g.n % 32 != 0) return fail(WQ4_ESHAPE, "tiled output needs N % 32 == 0");
   DeviceGuard dg(w->device);
   wq4::EpiArgs epi = make_epi(bias_dev, (flags & WQ4_EPI_RESIDUAL) ? residual_dev : nullptr, y_dev, (int)w->g.n,
@@ -689,10 +737,10 @@ wq4_status wq4_gemm_tiled_lnfold(const wq4_tensor* w, const float* bias_dev, con
   if (consumer) {
     epi.lnf_stats_in = fold->stats_in_dev;
     epi.lnf_wg = fold->wg_dev;
-    epi.lnf_tiles = (int)(w->g.k / 32);
+    epi.lnf_tiles = (int)(w->g.k / 16);
   }
   return gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, tiled_out ? wq4::kEpiTiled : wq4::kEpiF32,
-              ns_of(prec), static_cast<hipStream_t>(stream), true);
+              ns_of(prec), static_cast<hipStream_t>(stream), false, true);
 }
 
 wq4_status wq4_ln_fold_vectors(const wq4_tensor* w, const float* gamma, const float* beta, const float* bias,

@@ -57,4 +57,22 @@ hipError_t launch_q4_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* s
                           const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int ns, const DecodeWs* ws,
                           hipStream_t st, int wtype);
 
+// The decode-step GEMM (wq4_skinny.hip): rows <= 32, 16-column workgroups on
+// 16x16x32 MFMAs, one Q4 block per MFMA with the scale applied per block in
+// f32.  Its own weight layout (q16 / d16, or f16s for f16 weights) is built
+// at upload next to the prefill kernel's.  LayerNorm-fold statistics are per
+// 16-column tile (EpiArgs::lnf_tiles = K / 16), K <= 1280 for a consumer.
+inline int64_t skinny_units(const Q4Geom& g) { return (g.kb + 3) / 4; }
+inline size_t skinny_q_bytes(const Q4Geom& g) { return (size_t)(g.np / 16) * skinny_units(g) * 1024; }
+inline size_t skinny_d_bytes(const Q4Geom& g) { return (size_t)(g.np / 16) * skinny_units(g) * 128; }
+inline size_t skinny_f16_bytes(const Q4Geom& g) { return (size_t)(g.np / 16) * g.kb * 1024; }
+void repack_q4_skinny(const uint8_t* raw, const Q4Geom& g, uint32_t* q16, uint16_t* d16);
+void repack_f16_skinny(const uint16_t* w, const Q4Geom& g, uint16_t* f16s);
+bool skinny_supported(const Q4Geom& g, int rows);
+constexpr int kSkinnyMaxLnTiles = 80;  // LayerNorm-fold consumer: K / 16 tile statistics per row
+// ws: the stream's split-K workspace (partials + arrival counters) for the
+// K splits of large K (fc2).
+hipError_t launch_skinny_gemm(const Q4Geom& g, const uint32_t* wq, const uint16_t* wd, const _Float16* at, int rows,
+                              const EpiArgs& e, int epi_mode, int ns, int wtype, const DecodeWs* ws, hipStream_t st);
+
 }  // namespace wq4

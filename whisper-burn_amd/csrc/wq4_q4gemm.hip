@@ -398,6 +398,9 @@ __host__ __device__ constexpr size_t decode_lds_bytes_dev(int w) {
   return (size_t)(w == 8 ? w : w - 1) * 16 * 64 * 4 + (size_t)32 * kStageLd * 4;
 }
 
+#ifndef WQ4_DIAG
+#define WQ4_DIAG 0
+#endif
 template <int NS, int EPI, int PER, int MT, int W, int WK, bool LNA = false>
 __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* __restrict__ nib,
                                                               const uint32_t* __restrict__ sc,
@@ -458,6 +461,9 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
 
   // this wave's weights (once-read stream: nt) -- zeros past cnt
   const size_t t0 = (size_t)nt * nbp + bp0;
+  // WQ4_DIAG (timing diagnostics only, scripts/gpu_diag.sh; 0 in the product):
+  // 1 no MFMAs, 2 no A loads, 3 no weight loads, 4 no epilogue
+  constexpr int kDiag = WQ4_DIAG;
   constexpr int BW = WK == kWeightsF16 ? 4 : 1;  // 16 B weight loads per lane per bp
   const __amdgpu_buffer_rsrc_t rw = brsrc(nib + t0 * 1024 * BW, (uint32_t)cnt * 1024 * BW);
   u32x4 br[PER][BW];
@@ -473,8 +479,8 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
     const __amdgpu_buffer_rsrc_t rsc = brsrc(sc + t0 * 32, (uint32_t)cnt * 128);
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      br[i][0] = __builtin_amdgcn_raw_buffer_load_b128(rw, (i * 64 + lane) * 16, 0, 2);
-      bs[i] = __builtin_amdgcn_raw_buffer_load_b32(rsc, (i * 32 + r) * 4, 0, 2);
+      br[i][0] = kDiag == 3 ? u32x4{0u, 0u, 0u, 0u} : __builtin_amdgcn_raw_buffer_load_b128(rw, (i * 64 + lane) * 16, 0, 2);
+      bs[i] = kDiag == 3 ? 0u : __builtin_amdgcn_raw_buffer_load_b32(rsc, (i * 32 + r) * 4, 0, 2);
     }
   }
   // activation fragments of every m-tile, rows >= M read as zeros
@@ -566,7 +572,7 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
 #pragma unroll
             for (int q = 0; q < NS; ++q) {
               const int frag = ((2 * i + blk) * 2 + kk) * NS + q;
-              a[mt][i][blk][kk][q] = bload_h8<0>(ra, row_ok ? frag * 1024 + lane * 16 : kOob);
+              a[mt][i][blk][kk][q] = kDiag == 2 ? half8{} : bload_h8<0>(ra, row_ok ? frag * 1024 + lane * 16 : kOob);
             }
     }
   }
@@ -621,7 +627,7 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
     }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      if (i < cnt) {
+      if (kDiag != 1 && i < cnt) {
 #pragma unroll
         for (int blk = 0; blk < 2; ++blk) {
           half8 bh0, bl0, bh1, bl1;
@@ -650,6 +656,10 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = acc0[i] + acc1[i];
 
+    if constexpr (kDiag == 4) {  // diagnostics: no reduction / epilogue at all
+      if (acc[0] == 12345.0f) e.out[0] = acc[1];
+      return;
+    }
     if constexpr (W == 8) {
       // whole K in this workgroup: every wave finalises 2 of the 16
       // accumulator registers (same wave-order sum as the 4-wave path) and
