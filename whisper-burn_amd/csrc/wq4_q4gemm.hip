@@ -15,14 +15,19 @@
 //                   reduced through LDS in a fixed order; A rows beyond M are
 //                   never loaded.
 //
-// Arithmetic (both kernels, every output):  with x = x_hi + x_lo (f16 pair)
-// and the exact weight B = (q - 8) * d' = B_hi + B_lo (f16 pair, d' the
-// row-prescaled f16 scale, wq4_layout.hpp),
-//   acc += MFMA(x_hi, B_hi) + MFMA(x_lo, B_hi) + MFMA(x_hi, B_lo)
-// per 16-k half, in k order, f32 accumulation, then y = acc * 2^-s_n.  The
-// dropped x_lo * B_lo term is < 2^-22 relative.  WQ4_PREC_F16 keeps only
-// MFMA(x_hi, B_hi).  Per-row instruction order depends on (N, K) only, never
-// on M or the tile position: a row's result is identical at batch 1 and 256.
+// Arithmetic, x = x_hi + x_lo (f16 pair):
+//   prefill, Q4_0 weights -- block-scaled: per Q4 block t = sum over its 32 k
+//     of MFMA(x_hi, q - 8) + MFMA(x_lo, q - 8) (q - 8 exact in f16, f32
+//     accumulation from zero), acc = t * d' + acc, then y = acc * 2^-s_n:
+//     two MFMAs per multiply-add;
+//   decode, and f16 weights -- with the exact weight B = (q - 8) * d' = B_hi +
+//     B_lo (f16 pair, d' the row-prescaled f16 scale, wq4_layout.hpp),
+//     acc += MFMA(x_hi, B_hi) + MFMA(x_lo, B_hi) + MFMA(x_hi, B_lo) per 16-k
+//     half (f16 weights: B_lo = 0), f32 accumulation; the dropped x_lo * B_lo
+//     term is < 2^-22 relative.
+// WQ4_PREC_F16 keeps only the x_hi terms.  Per-row instruction order depends
+// on (N, K) only, never on M or the tile position: a row's result is
+// identical at batch 1 and 256.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -216,34 +221,53 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
       const uint8_t* abuf = smem + (bp & 1) * BUF;
 #pragma unroll
       for (int blk = 0; blk < 2; ++blk) {
-        half8 bh[TN][2], bl[TN][2];
+        if constexpr (WK == kWeightsF16) {
+          // exact f16 weights: acc += x_hi * w + x_lo * w per 16-k half
 #pragma unroll
-        for (int nt = 0; nt < TN; ++nt) {
-          if constexpr (WK == kWeightsF16) {
+          for (int mt = 0; mt < TM; ++mt) {
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk) bh[nt][kk] = __builtin_bit_cast(half8, braw[nt][blk * 2 + kk]);
-          } else {
-            const uint32_t dbits = blk ? (bsc[nt] >> 16) : (bsc[nt] & 0xffffu);
+            for (int kk = 0; kk < 2; ++kk) {
+              const uint8_t* fa = abuf + mt * CHUNK + ((blk * 2 + kk) * NS) * 1024 + lane * 16;
+              const half8 ahi = *reinterpret_cast<const half8*>(fa);
+              half8 alo;
+              if constexpr (NS == 2) alo = *reinterpret_cast<const half8*>(fa + 1024);
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk)
-              deq_scaled<NS>(braw[nt][0][blk * 2 + kk], dbits, bh[nt][kk], bl[nt][kk]);
+              for (int nt = 0; nt < TN; ++nt) {
+                const half8 bw = __builtin_bit_cast(half8, braw[nt][blk * 2 + kk]);
+                acc[mt][nt] = mfma32(ahi, bw, acc[mt][nt]);
+                if constexpr (NS == 2) acc[mt][nt] = mfma32(alo, bw, acc[mt][nt]);
+              }
+            }
           }
-        }
+        } else {
+          // Q4_0, block-scaled: t = sum over the block's 32 k of x * (q - 8)
+          // (exact f16 integers, f32 MFMA accumulation from zero), then
+          // acc += t * d' -- two MFMAs per multiply-add with NS = 2 instead
+          // of three for an f16-pair weight
+          half8 qf[TN][2];
+          float dsc[TN];
 #pragma unroll
-        for (int mt = 0; mt < TM; ++mt) {
+          for (int nt = 0; nt < TN; ++nt) {
 #pragma unroll
-          for (int kk = 0; kk < 2; ++kk) {
-            const uint8_t* fa = abuf + mt * CHUNK + ((blk * 2 + kk) * NS) * 1024 + lane * 16;
-            const half8 ahi = *reinterpret_cast<const half8*>(fa);
-            half8 alo;
-            if constexpr (NS == 2) alo = *reinterpret_cast<const half8*>(fa + 1024);
+            for (int kk = 0; kk < 2; ++kk) qf[nt][kk] = deq8(braw[nt][0][blk * 2 + kk]);
+            dsc[nt] = (float)__builtin_bit_cast(_Float16, (uint16_t)(blk ? (bsc[nt] >> 16) : (bsc[nt] & 0xffffu)));
+          }
+#pragma unroll
+          for (int mt = 0; mt < TM; ++mt) {
+            const uint8_t* fa = abuf + mt * CHUNK + (blk * 2 * NS) * 1024 + lane * 16;
+            half8 ahi[2], alo[2];
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+              ahi[kk] = *reinterpret_cast<const half8*>(fa + kk * NS * 1024);
+              if constexpr (NS == 2) alo[kk] = *reinterpret_cast<const half8*>(fa + kk * NS * 1024 + 1024);
+            }
 #pragma unroll
             for (int nt = 0; nt < TN; ++nt) {
-              acc[mt][nt] = mfma32(ahi, bh[nt][kk], acc[mt][nt]);
-              if constexpr (NS == 2) {
-                acc[mt][nt] = mfma32(alo, bh[nt][kk], acc[mt][nt]);
-                if constexpr (WK != kWeightsF16) acc[mt][nt] = mfma32(ahi, bl[nt][kk], acc[mt][nt]);
-              }
+              floatx16 t = mfma32(ahi[0], qf[nt][0], floatx16{});
+              if constexpr (NS == 2) t = mfma32(alo[0], qf[nt][0], t);
+              t = mfma32(ahi[1], qf[nt][1], t);
+              if constexpr (NS == 2) t = mfma32(alo[1], qf[nt][1], t);
+              acc[mt][nt] = t * dsc[nt] + acc[mt][nt];
             }
           }
         }
@@ -912,29 +936,35 @@ DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal) {
   return p;
 }
 
-__global__ __launch_bounds__(1024) void act_scale_kernel(const float* __restrict__ x, int M, int K, int ld,
-                                                         float* __restrict__ out) {
-  __shared__ float red[16];
+__global__ __launch_bounds__(256) void act_max_kernel(const float* __restrict__ x, int M, int K, int ld,
+                                                      unsigned* __restrict__ max_bits) {
   float mx = 0.0f;
-  for (int64_t i = threadIdx.x; i < (int64_t)M * K; i += 1024) {
-    const int64_t m = i / K;
-    mx = fmaxf(mx, fabsf(x[m * ld + (i - m * K)]));
-  }
+  for (int m = blockIdx.x; m < M; m += gridDim.x)
+    for (int c = threadIdx.x; c < K; c += 256) mx = fmaxf(mx, fabsf(x[(size_t)m * ld + c]));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < 16; ++w) mx = fmaxf(mx, red[w]);
-    int e = 4;  // the internal producers' 2^4, unless the range needs less
-    if (mx > 0.0f && mx < INFINITY) e = min(4, (int)floorf(log2f(16384.0f / mx)));
-    out[0] = ldexpf(1.0f, e);
-    out[1] = ldexpf(1.0f, -e);
-  }
+  // |x| >= 0: the f32 bit patterns order like the values, so an unsigned
+  // maximum (a vector atomic, order-independent) gives the exact maximum
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_max(max_bits, __float_as_uint(mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void act_scale_finish_kernel(float* __restrict__ out) {
+  const float mx = __uint_as_float(reinterpret_cast<const unsigned*>(out)[2]);
+  int e = 4;  // the internal producers' 2^4, unless the range needs less
+  if (mx > 0.0f && mx < INFINITY) e = min(4, (int)floorf(log2f(16384.0f / mx)));
+  out[0] = ldexpf(1.0f, e);
+  out[1] = ldexpf(1.0f, -e);
 }
 
 hipError_t launch_act_scale(const float* x, int M, int K, int ld, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(act_scale_kernel, dim3(1), dim3(1024), 0, st, x, M, K, ld, out);
+  // out[2] holds the running maximum's bits; zeroed per call on the stream
+  hipError_t e = hipMemsetAsync(out + 2, 0, sizeof(unsigned), st);
+  if (e != hipSuccess) return e;
+  const int grid = M < 2048 ? (M < 1 ? 1 : M) : 2048;
+  hipLaunchKernelGGL(act_max_kernel, dim3(grid), dim3(256), 0, st, x, M, K, ld,
+                     reinterpret_cast<unsigned*>(out + 2));
+  hipLaunchKernelGGL(act_scale_finish_kernel, dim3(1), dim3(1), 0, st, out);
   return hipGetLastError();
 }
 

@@ -150,7 +150,8 @@ def get_precision() -> int:
 
 
 def set_kernel_policy(policy: int) -> None:
-    """0 = automatic, 1 = MFMA tile ("prefill") kernel, 2 = K-split ("decode") kernel."""
+    """0 = automatic, 1 = MFMA tile ("prefill") kernel, 2 = K-split ("decode")
+    kernel, 3 = decode-step kernel (include/wq4.h)."""
     check(lib().wq4_set_kernel_policy(policy))
 
 
