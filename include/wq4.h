@@ -179,8 +179,9 @@ wq4_status wq4_gemm_ln_tiled(const wq4_tensor* w, const float* bias_dev, const f
                              void* at_out_dev, int64_t rows, unsigned flags, wq4_precision prec, int kernel,
                              void* stream);
 
-/* LayerNorm folded into the decoder GEMMs around it (the decode-step
- * kernel: rows <= 32, K % 128 == 0, N % 16 == 0; replaces the wq4_layernorm launch between a
+/* LayerNorm folded into the decoder GEMMs around it (rows <= 32: the
+ * 8-wave decode kernel where its 8-wave plan applies, else -- or under
+ * kernel policy 3 -- the decode-step kernel; replaces the wq4_layernorm launch between a
  * residual GEMM and the GEMM that reads LayerNorm of its output -- the
  * attn_ln / cross_attn_ln / mlp_ln -> Q4Linear pairs of decoder.rs:77-112).
  * LN(x) = (x - mean) / sqrt(var + 1e-5) * gamma + beta (layers.rs:12-32), so

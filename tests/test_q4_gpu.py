@@ -461,10 +461,12 @@ def test_f16_weights_batch_invariance(torch, policy):
 @pytest.mark.parametrize("prec", [0, 1])
 @pytest.mark.parametrize("m", [1, 7, 16, 32])
 @pytest.mark.parametrize("n2,flags", [(1280, 0), (5120, 1)])
-def test_ln_fold_matches_layernorm_path(torch, wtype, prec, m, n2, flags):
+@pytest.mark.parametrize("kern", [3, 2])
+def test_ln_fold_matches_layernorm_path(torch, wtype, prec, m, n2, flags, kern):
     """wq4_gemm_tiled_lnfold: a residual GEMM x = r + W1 a + b1 that also
-    emits tiled(x * gamma) and 16-column tile statistics (producer; the
-    decode-step kernel, rows <= 32), then a GEMM on
+    emits tiled(x * gamma) and 16-column tile statistics (producer; rows <=
+    32: the 8-wave decode kernel, kern 2 -- the model's choice -- or the
+    decode-step kernel, kern 3), then a GEMM on
     LayerNorm(x) (consumer, decoder.rs:77-112 attn_ln -> query etc.),
     against wq4_gemm_tiled -> wq4_layernorm -> wq4_gemm_tiled.  The
     producer's x is bit-identical; the consumer re-associates
@@ -490,6 +492,7 @@ def test_ln_fold_matches_layernorm_path(torch, wtype, prec, m, n2, flags):
     g = rng.uniform(0.8, 1.2, d).astype(np.float32)
     be = rng.uniform(-0.1, 0.1, d).astype(np.float32)
     L = wq4.lib()
+    wq4.set_kernel_policy(kern)
     assert L.wq4_lnfold_supported(w1.handle, m) == 1 and L.wq4_lnfold_supported(w2.handle, m) == 1
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
@@ -501,7 +504,7 @@ def test_ln_fold_matches_layernorm_path(torch, wtype, prec, m, n2, flags):
 
     # reference: residual GEMM, LayerNorm kernel, GEMM
     x_ref = res.clone()
-    wq4.check(L.wq4_gemm_tiled(w1.handle, p(b1), p(at_a), p(x_ref), p(x_ref), None, m, 2, prec, 3, st))
+    wq4.check(L.wq4_gemm_tiled(w1.handle, p(b1), p(at_a), p(x_ref), p(x_ref), None, m, 2, prec, kern, st))
     at_ln = torch.zeros(L.wq4_atiled_bytes(m, d, prec), dtype=torch.uint8, device="cuda:0")
     wq4.check(L.wq4_layernorm(p(x_ref), p(gd), p(bed), m, d, prec, p(at_ln), None, st))
     ob = L.wq4_atiled_bytes(m, n2, prec)

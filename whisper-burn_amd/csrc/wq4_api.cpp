@@ -180,6 +180,21 @@ int pick_kernel(const wq4_tensor* w, int64_t rows, int kernel) {
   return use_decode(rows) ? 2 : 1;
 }
 
+// The kernel of a LayerNorm-fold GEMM (16-column tile statistics, K <= 1280
+// for a consumer): the 8-wave decode kernel (2) where its 8-wave plan applies
+// -- in the model's decode step, two groups' chains run concurrently and its
+// 40-160 workgroup grids left room for the other group's kernels: decode
+// 875 ms against 905-914 ms with the decode-step kernel's 80-240 workgroups
+// (Large-V3, 32 clips, scripts/gpu_ab_lnfold.sh, r02) -- else the decode-step
+// kernel (3), which policy 3 also forces; 0 = unsupported.
+int lnfold_kernel(const wq4_tensor* w, int64_t rows) {
+  if (!w || w->flat || rows < 1 || rows > 32) return 0;
+  const bool old_ok = wq4::decode_ln_supported(w->g, (int)rows);
+  if (g_policy.load() == 3) return skinny_ok(w, rows) ? 3 : 0;
+  if (old_ok) return 2;
+  return skinny_ok(w, rows) ? 3 : 0;
+}
+
 wq4_status gemm(const wq4_tensor* w, const _Float16* at, int64_t rows, const wq4::EpiArgs& e, int mode, int ns,
                 hipStream_t st, bool dec, bool skinny = false) {
   if (skinny) {
@@ -695,10 +710,7 @@ wq4_status wq4_gemm_ln_tiled(const wq4_tensor* w, const float* bias_dev, const f
                         flags & ~WQ4_EPI_LN_FUSED, prec, kernel, stream);
 }
 
-int wq4_lnfold_supported(const wq4_tensor* w, int64_t rows) {
-  if (!w || w->flat || rows < 1) return 0;
-  return skinny_ok(w, rows) ? 1 : 0;  // the decode-step kernel's 16-column tile statistics
-}
+int wq4_lnfold_supported(const wq4_tensor* w, int64_t rows) { return lnfold_kernel(w, rows) != 0 ? 1 : 0; }
 
 wq4_status wq4_gemm_tiled_lnfold(const wq4_tensor* w, const float* bias_dev, const void* at_dev,
                                  const float* residual_dev, float* y_dev, void* at_out_dev, int64_t rows,
@@ -709,8 +721,9 @@ wq4_status wq4_gemm_tiled_lnfold(const wq4_tensor* w, const float* bias_dev, con
   if (s != WQ4_OK) return s;
   if (!fold) return fail(WQ4_EINVAL, "fold is null");
   if (rows == 0) return WQ4_OK;
-  if (!wq4_lnfold_supported(w, rows))
-    return fail(WQ4_ESHAPE, "LayerNorm fold needs the decode-step kernel (rows <= 32, K % 128 == 0, N % 16 == 0)");
+  const int kk = lnfold_kernel(w, rows);
+  if (kk == 0)
+    return fail(WQ4_ESHAPE, "LayerNorm fold needs rows <= 32 and the decode-step or 8-wave decode kernel");
   const bool tiled_out = (flags & WQ4_EPI_TILED_OUT) != 0;
   const bool producer = fold->at_out_dev != nullptr, consumer = fold->stats_in_dev != nullptr;
   if (!at_dev || (tiled_out ? !at_out_dev : !y_dev)) return fail(WQ4_EINVAL, "null argument");
@@ -740,7 +753,7 @@ wq4_status wq4_gemm_tiled_lnfold(const wq4_tensor* w, const float* bias_dev, con
     epi.lnf_tiles = (int)(w->g.k / 16);
   }
   return gemm(w, static_cast<const _Float16*>(at_dev), rows, epi, tiled_out ? wq4::kEpiTiled : wq4::kEpiF32,
-              ns_of(prec), static_cast<hipStream_t>(stream), false, true);
+              ns_of(prec), static_cast<hipStream_t>(stream), kk == 2, kk == 3);
 }
 
 wq4_status wq4_ln_fold_vectors(const wq4_tensor* w, const float* gamma, const float* beta, const float* bias,

@@ -24,11 +24,12 @@ struct EpiArgs {
   const float* lng;
   const float* lnb;
   int lnd;
-  // LayerNorm folded into the GEMMs around it (decode kernel, 8-wave plans;
-  // wq4_gemm_tiled_lnfold).  Producer (a residual GEMM whose output x feeds
-  // LayerNorm(x; gamma, beta)): also writes the A-tiled operand of x * gamma
-  // (lnf_at, K' = N, lnf_nbp block pairs) and per (row, 32-column tile) the
-  // tile mean and sum of squared deviations (lnf_stats_out [M][N/32][2]).
+  // LayerNorm folded into the GEMMs around it (decode-step kernel, or the
+  // decode kernel's 8-wave plans; wq4_gemm_tiled_lnfold).  Producer (a
+  // residual GEMM whose output x feeds LayerNorm(x; gamma, beta)): also
+  // writes the A-tiled operand of x * gamma (lnf_at, K' = N, lnf_nbp block
+  // pairs) and per (row, 16-column tile) the tile mean and sum of squared
+  // deviations (lnf_stats_out [M][N/16][2]).
   // Consumer (a GEMM on LayerNorm(x)): A = tiled(x * gamma); merges the
   // lnf_tiles tile statistics of each row (Chan et al.) and applies
   // out = (acc - mean * lnf_wg[n]) / sqrt(var + 1e-5) + bias[n] before the

@@ -467,7 +467,7 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
   // LayerNorm fold, consumer: thread (row tid / 16, part tid % 16) loads the
   // row's tile statistics j = part, part + 16, ... first, so they land before
   // the weight / operand stream; merged below while that stream is in flight.
-  constexpr int kLnfPer = 4;  // <= 64 tiles (D <= 2048)
+  constexpr int kLnfPer = 5;  // <= 80 16-column tiles (D <= 1280)
   floatx2 lnf_st[kLnfPer];
   const int lnf_row = tid >> 4, lnf_part = tid & 15;
   if constexpr (W == 8) {
@@ -614,9 +614,9 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
 #pragma unroll
       for (int u = 0; u < kLnfPer; ++u) {
         if (lnf_part + 16 * u < e.lnf_tiles) {
-          const float n = n_a + 32.0f, d = lnf_st[u][0] - m_a;
-          m_a = m_a + d * (32.0f / n);
-          q_a = q_a + lnf_st[u][1] + d * d * (n_a * 32.0f / n);
+          const float n = n_a + 16.0f, d = lnf_st[u][0] - m_a;
+          m_a = m_a + d * (16.0f / n);
+          q_a = q_a + lnf_st[u][1] + d * d * (n_a * 16.0f / n);
           n_a = n;
         }
       }
@@ -636,7 +636,7 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
       }
       if (lnf_part == 0) {
         lnf_mu[lnf_row] = m_a;
-        lnf_den[lnf_row] = sqrtf(q_a / (float)(32 * e.lnf_tiles) + 1e-5f);
+        lnf_den[lnf_row] = sqrtf(q_a / (float)(16 * e.lnf_tiles) + 1e-5f);
       }
     }
   }
@@ -765,20 +765,20 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
             e2.out_tiled = e.lnf_at;
             e2.nbp_next = e.lnf_nbp;
             store_tiled_slab<NS, 1>(stage, e2, mt0 + mt, nt, lane);
-          } else if (wave == 1 && lane < 32) {
-            const int row = (mt0 + mt) * 32 + lane;
+          } else if (wave == 1) {  // lane (row, half): the 16-column tile statistics
+            const int rl = lane & 31, hf = lane >> 5, row = (mt0 + mt) * 32 + rl;
             if (row < e.m) {
               float sum = 0.0f;
 #pragma unroll
-              for (int c = 0; c < 32; ++c) sum += lnf_x[lane * 33 + c];
-              const float mean = sum * (1.0f / 32.0f);
+              for (int c = 0; c < 16; ++c) sum += lnf_x[rl * 33 + 16 * hf + c];
+              const float mean = sum * (1.0f / 16.0f);
               float m2 = 0.0f;
 #pragma unroll
-              for (int c = 0; c < 32; ++c) {
-                const float d = lnf_x[lane * 33 + c] - mean;
+              for (int c = 0; c < 16; ++c) {
+                const float d = lnf_x[rl * 33 + 16 * hf + c] - mean;
                 m2 += d * d;
               }
-              *reinterpret_cast<floatx2*>(e.lnf_stats_out + ((size_t)row * (e.n / 32) + nt) * 2) =
+              *reinterpret_cast<floatx2*>(e.lnf_stats_out + ((size_t)row * (e.n / 16) + 2 * nt + hf) * 2) =
                   floatx2{mean, m2};
             }
           }

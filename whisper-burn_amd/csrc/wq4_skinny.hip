@@ -148,6 +148,8 @@ __device__ __forceinline__ void sk_load(SkBlock<NT, MT, NS, WK>& B, int b, int l
       B.d[t] = (float)__builtin_bit_cast(_Float16, db);
     }
   }
+  // (weights and scales with the default cache policy: non-temporal loads
+  // measured 3 % slower over the decode step, r02 chain trace)
   // A-tiled (32x32x16 fragment) layout read as 16x16x32 fragments: lane
   // (r, g) = row 16 mt + r, k = 32 b + 8 g .. + 7 -> fragment (b, kk = g >> 1),
   // lane' = row + 32 (g & 1).  Rows >= m are not read (zeros).
