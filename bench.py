@@ -17,9 +17,13 @@ roofline: the dominant kernel by time per step -- the Q4 GEMMs (north-star
 kernel, MFMA tile kernel, timed live with HIP events on their launch stream
 during the timed steps; algorithmic FLOPs = 2*M*N*K per launch) or the decode
 step's cross-attention (HBM stream of every clip's encoder output, f16 hi/lo
-planes, shared by all heads -- no per-layer K/V caches; HIP-event timed by
-wa_probe_kernels right after the timed steps; algorithmic bytes = encoder
-planes + raw Wk, Wv + operands).  Both, and the decode-step fc1 GEMM, are reported.
+planes, shared by all heads -- no per-layer K/V caches; algorithmic bytes =
+encoder planes + raw Wk, Wv + operands).  The cross-attention is HIP-event
+timed by wa_probe_kernels right after the timed steps at the shape the decode
+graphs run it (one decode group's clips, wa_decode_group_rows), and carries
+the in-graph durations of the same grids from the committed rocprofv3 chain
+trace (profiles/xattn_in_graph.json, scripts/in_graph_summary.py) as a
+cross-check.  Both, and the decode-step fc1 GEMM, are reported.
 
 cpu_baseline: the reference's CPU dequant->GEMM path
 (src/gguf/tests.rs:60-87,172-184, restated in oracle/q4_oracle.c) on
@@ -136,6 +140,28 @@ def pmc_traffic_xattn_probe(rows: int, heads: int, d_model: int, workload: dict)
              pmc_traffic_grid("xattn_main_kernel", 8 * 512 * rows, workload),
              pmc_traffic_grid("xattn_out_kernel", heads * 512 * ((rows + 3) // 4), workload)]
     return None if any(p is None for p in parts) else sum(parts)
+
+
+def in_graph_xattn(rows: int, heads: int, d_model: int, workload: dict):
+    """Sum of the in-graph average durations (us) of xattn_q, xattn_main and
+    xattn_out at the decode group's grids, from the committed chain trace
+    (profiles/xattn_in_graph.json) of this workload, or None."""
+    try:
+        with open(os.path.join(REPO, "profiles", "xattn_in_graph.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != workload:
+        return None
+    want = {"xattn_q_mfma_kernel": [2560, heads, (rows + 31) // 32], "xattn_main_kernel": [4096, rows, 1],
+            "xattn_out_kernel": [10240, (rows + 3) // 4, 1]}
+    tot = 0.0
+    for k, grid in want.items():
+        hit = [e for e in d.get("kernels", []) if e["kernel"] == k and list(e["grid"]) == grid]
+        if not hit:
+            return None
+        tot += hit[0]["avg_us"]
+    return tot
 
 
 def cpu_threads() -> int:
@@ -345,7 +371,8 @@ def main() -> None:
     clips = world * B * args.steps
     value = job_rtf(world, B, args.steps, elapsed)
 
-    probe = model.probe_kernels(B, iters=20) if rank == 0 else None
+    group_rows = whisper_amd.decode_group_rows(B)
+    probe = model.probe_kernels(group_rows, iters=20) if rank == 0 else None
     if rank == 0:
         workload = {"variant": args.variant, "weights": args.weights, "precision": args.precision, "clips": B}
         q4 = prof["q4_gemm"]
@@ -362,18 +389,23 @@ def main() -> None:
         # decode phase: cross-attention (HBM stream of the cached K/V), probed after the timed steps
         xa = probe["cross_attention"]
         xa_gbs = xa["bytes"] / (xa["us"] * 1e-6) * 1e-9
+        groups = -(-B // group_rows)
+        ig = in_graph_xattn(group_rows, cfg["n_text_head"], cfg["n_text_state"], workload)
         roof_xa = {"bound": "hbm", "achieved": round(xa_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                    "frac": round(xa_gbs / PEAK_HBM_GBS, 4),
-                   "traffic": pmc_traffic_xattn_probe(B, cfg["n_text_head"], cfg["n_text_state"], workload),
-                   "kernel": "cross-attention over the encoder output: xattn_q + xattn_main + xattn_out "
-                             "(split merge fused; decode step, Tq = 1)", "avg_us": round(xa["us"], 2),
-                   "bytes_per_launch": xa["bytes"],
-                   "total_ms_per_step": round(xa["us"] * 1e-3 * cfg["n_text_layer"] * steps_run, 2)}
+                   "traffic": pmc_traffic_xattn_probe(group_rows, cfg["n_text_head"], cfg["n_text_state"], workload),
+                   "kernel": f"cross-attention over the encoder output: xattn_q + xattn_main + xattn_out "
+                             f"(decode step, Tq = 1, {group_rows} clips per launch = one of {groups} decode groups)",
+                   "avg_us": round(xa["us"], 2), "bytes_per_launch": xa["bytes"],
+                   "in_graph_avg_us": None if ig is None else round(ig, 2),
+                   "in_graph_frac": None if ig is None else round(xa["bytes"] / (ig * 1e-6) * 1e-9 / PEAK_HBM_GBS, 4),
+                   "total_ms_per_step": round(xa["us"] * 1e-3 * cfg["n_text_layer"] * steps_run * groups, 2)}
         dq = probe["decode_fc1"]
         roof_dq = {"bound": "hbm", "achieved": round(dq["bytes"] / (dq["us"] * 1e-6) * 1e-9, 1),
                    "peak": PEAK_HBM_GBS, "unit": "GB/s",
                    "frac": round(dq["bytes"] / (dq["us"] * 1e-6) * 1e-9 / PEAK_HBM_GBS, 4), "traffic": None,
-                   "kernel": "q4_gemm_decode_kernel (decode-step fc1, split-K)", "avg_us": round(dq["us"], 2),
+                   "kernel": f"q4_gemm_decode_kernel (decode-step fc1, split-K, {group_rows} rows)",
+                   "avg_us": round(dq["us"], 2),
                    "tflops": round(dq["flops"] / (dq["us"] * 1e-6) * 1e-12, 2)}
         dominant = roof_xa if roof_xa["total_ms_per_step"] > roof_q4["total_ms_per_step"] else roof_q4
         line = {

@@ -1323,6 +1323,12 @@ wq4_status wa_transcribe_trace(wa_model* m, const float* mel_dev, int n_clips, i
   return s;
 }
 
+int wa_decode_group_rows(int n_clips) {
+  if (n_clips < 1) return 0;
+  const int G = decode_groups(n_clips);
+  return (n_clips + G - 1) / G;  // the largest group (groups split [0, B) evenly, transcribe_batch)
+}
+
 wq4_status wa_probe_kernels(wa_model* m, int n_clips, int iters, double* out) {
   if (!m || !out) return fail(WQ4_EINVAL, "null argument");
   if (n_clips < 1 || n_clips > m->bmax || iters < 1) return fail(WQ4_EINVAL, "bad n_clips / iters");

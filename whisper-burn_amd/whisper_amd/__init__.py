@@ -47,6 +47,8 @@ def lib() -> ctypes.CDLL:
         L.wa_profile_enable.argtypes = [vp, c_int]
         L.wa_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), c_int]
         L.wa_probe_kernels.argtypes = [vp, c_int, c_int, ctypes.POINTER(ctypes.c_double)]
+        L.wa_decode_group_rows.argtypes = [c_int]
+        L.wa_decode_group_rows.restype = c_int
         L.wa_model_create_synthetic_ex.argtypes = [c_int, c_int, ctypes.c_uint64, c_int, c_int, c_int,
                                                    ctypes.POINTER(vp)]
         L.wa_model_weight_type.argtypes = [vp]
@@ -73,6 +75,7 @@ def lib() -> ctypes.CDLL:
         for n in ("wa_xattn_check", "wa_transcribe_trace", "wa_encoder_attention_check", "wa_self_attention_check",
                   "wa_logits_argmax_check", "wa_log_mel", "wa_mel_filterbank", "wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
                   "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read", "wa_probe_kernels",
+                  "wa_decode_group_rows",
                   "wa_model_create_from_gguf", "wa_model_create_synthetic_ex", "wa_gguf_open", "wa_gguf_tensor_info", "wa_gguf_tensor_data"):
             getattr(L, n).restype = c_int
         _lib = L
@@ -82,6 +85,12 @@ def lib() -> ctypes.CDLL:
 def check(st: int) -> None:
     if st != 0:
         raise wq4.WQ4Error(st, lib().wa_last_error().decode(errors="replace"))
+
+
+def decode_group_rows(n_clips: int) -> int:
+    """Clips in the largest decode group of a transcribe batch of n_clips:
+    the row count of every captured decode-step launch (wa_decode_group_rows)."""
+    return int(lib().wa_decode_group_rows(n_clips))
 
 
 def synth_uniform(seed: int, name: str, n: int, lo: float, hi: float) -> np.ndarray:
