@@ -55,7 +55,14 @@ constexpr float kWkScale = 4096.0f, kXqInv = 1.0f / (16.0f * 4096.0f);
 constexpr float kQtScale = 32.0f, kEncScale = 32.0f, kSInv = 1.0f / 1024.0f;
 constexpr float kPScale = 32768.0f, kZInv = 1.0f / (32768.0f * 32.0f);
 constexpr float kZnScale = 32.0f, kWvScale = 4096.0f, kOutInv = 1.0f / (32.0f * 4096.0f);
-constexpr int kXattnSplits = 8;  // frame ranges per query row (measured: 8 beat 4, 6, 12 and 16)
+#ifndef WA_XATTN_SPLITS  // compile-time only: tuning builds of scripts/gpu_xattn_splits.sh
+#define WA_XATTN_SPLITS 8
+#endif
+// Frame ranges per query row.  Measured: 8 beat 4, 6, 12 and 16 in round 1;
+// in round 2's model (two concurrent decode groups of 16 clips) 12 and 16 ran
+// the isolated 16-clip launch faster (50.5 us vs 55.7 at 12) but the decode
+// slower (926 / 1073 ms vs 873): more workgroups crowd out the other group.
+constexpr int kXattnSplits = WA_XATTN_SPLITS;
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
