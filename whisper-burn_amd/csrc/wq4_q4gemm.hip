@@ -252,6 +252,18 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
             for (int kk = 0; kk < 2; ++kk) qf[nt][kk] = deq8(braw[nt][0][blk * 2 + kk]);
             dsc[nt] = (float)__builtin_bit_cast(_Float16, (uint16_t)(blk ? (bsc[nt] >> 16) : (bsc[nt] & 0xffffu)));
           }
+          // two temporaries in flight: tile (mt, 1)'s MFMA chain runs under
+          // the scale FMAs of (mt, 0), and (mt + 1, 0)'s under those of
+          // (mt, 1), so no FMA waits on the MFMA it reads
+          static_assert(TN == 2, "the interleave below pairs the two n-tiles of a wave");
+          floatx16 t0, t1;
+          auto chain = [&](const half8 (&ah)[2], const half8 (&al)[2], int nt) {
+            floatx16 t = mfma32(ah[0], qf[nt][0], floatx16{});
+            if constexpr (NS == 2) t = mfma32(al[0], qf[nt][0], t);
+            t = mfma32(ah[1], qf[nt][1], t);
+            if constexpr (NS == 2) t = mfma32(al[1], qf[nt][1], t);
+            return t;
+          };
 #pragma unroll
           for (int mt = 0; mt < TM; ++mt) {
             const uint8_t* fa = abuf + mt * CHUNK + (blk * 2 * NS) * 1024 + lane * 16;
@@ -261,15 +273,19 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
               ahi[kk] = *reinterpret_cast<const half8*>(fa + kk * NS * 1024);
               if constexpr (NS == 2) alo[kk] = *reinterpret_cast<const half8*>(fa + kk * NS * 1024 + 1024);
             }
+            t0 = chain(ahi, alo, 0);
+            if (mt > 0) acc[mt - 1][1] = t1 * dsc[1] + acc[mt - 1][1];
+            t1 = chain(ahi, alo, 1);
+            acc[mt][0] = t0 * dsc[0] + acc[mt][0];
+            // issue order: the m-tile's 4 A reads, then MFMA / 2 VALU pairs
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * NS, 0);
 #pragma unroll
-            for (int nt = 0; nt < TN; ++nt) {
-              floatx16 t = mfma32(ahi[0], qf[nt][0], floatx16{});
-              if constexpr (NS == 2) t = mfma32(alo[0], qf[nt][0], t);
-              t = mfma32(ahi[1], qf[nt][1], t);
-              if constexpr (NS == 2) t = mfma32(alo[1], qf[nt][1], t);
-              acc[mt][nt] = t * dsc[nt] + acc[mt][nt];
+            for (int i = 0; i < 4 * NS; ++i) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
             }
           }
+          acc[TM - 1][1] = t1 * dsc[1] + acc[TM - 1][1];
         }
       }
     }
