@@ -399,6 +399,10 @@ constexpr int kDecodeMaxKs = 8;  // K slices per n-tile (fix-up keeps all slabs 
 // zeros, so masked rows and the ragged end of a wave's K range need no exec
 // branches (which would make the compiler drain vmcnt between load groups).
 constexpr int kOob = 0x7fffff00;
+#ifndef WQ4_WEIGHT_AUX  // compile-time only (tuning builds): cache policy of the decode weight stream
+#define WQ4_WEIGHT_AUX 2  // nt
+#endif
+constexpr int kWeightAux = WQ4_WEIGHT_AUX;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
@@ -512,15 +516,15 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) br[i][q] = __builtin_amdgcn_raw_buffer_load_b128(rw, (i * 64 + lane) * 64 + q * 16, 0, 2);
+      for (int q = 0; q < 4; ++q) br[i][q] = __builtin_amdgcn_raw_buffer_load_b128(rw, (i * 64 + lane) * 64 + q * 16, 0, kWeightAux);
       bs[i] = 0;
     }
   } else {
     const __amdgpu_buffer_rsrc_t rsc = brsrc(sc + t0 * 32, (uint32_t)cnt * 128);
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      br[i][0] = kDiag == 3 ? u32x4{0u, 0u, 0u, 0u} : __builtin_amdgcn_raw_buffer_load_b128(rw, (i * 64 + lane) * 16, 0, 2);
-      bs[i] = kDiag == 3 ? 0u : __builtin_amdgcn_raw_buffer_load_b32(rsc, (i * 32 + r) * 4, 0, 2);
+      br[i][0] = kDiag == 3 ? u32x4{0u, 0u, 0u, 0u} : __builtin_amdgcn_raw_buffer_load_b128(rw, (i * 64 + lane) * 16, 0, kWeightAux);
+      bs[i] = kDiag == 3 ? 0u : __builtin_amdgcn_raw_buffer_load_b32(rsc, (i * 32 + r) * 4, 0, kWeightAux);
     }
   }
   // activation fragments of every m-tile, rows >= M read as zeros
