@@ -11,11 +11,13 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import wq4  # noqa: E402
 
 M = int(os.environ.get("ROWS", "48000"))
-POLICY = int(os.environ.get("POLICY", "0"))  # 4 = the f16-pair-weight tile kernel
+POLICY = int(os.environ.get("POLICY", "0"))  # kernel policy (include/wq4.h)
+PREC = int(os.environ.get("PREC", "0"))  # 0 = f16x2 (default), 1 = f16
 REPS = int(os.environ.get("REPS", "5"))
 SHAPES = [(3840, 1280), (1280, 1280), (5120, 1280), (1280, 5120)]
 rng = np.random.default_rng(0)
 wq4.set_kernel_policy(POLICY)
+wq4.set_precision(PREC)
 for N, K in SHAPES:
     w = rng.standard_normal((N, K)).astype(np.float32) * 0.05
     t = wq4.Q4Tensor.from_q4_bytes(wq4.quantize_q4_0(w), (N, K))

@@ -425,6 +425,40 @@ def test_gemm_ln_fused_bit_exact(torch, wtype, prec, m, n, flags):
     assert np.array_equal(outs[0].view(np.uint32) if not tiled else outs[0], outs[1].view(np.uint32) if not tiled else outs[1])
 
 
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("m,d", [(1, 1280), (31, 1280), (33, 384), (100, 160), (70, 96), (40, 2048), (3000, 1280),
+                                 (2049, 96), (4100, 2048), (3001, 160)])
+def test_layernorm_tiled_equals_f32_then_tile(torch, prec, m, d):
+    """wq4_layernorm's A-tiled output (one wave per row up to 2048 rows, then
+    layernorm_tiled_kernel: rows in registers, 1 KiB fragment stores) equals
+    the f32 LayerNorm rows tiled by
+    wq4_tile_activations bit for bit -- including the zero rows / columns that
+    pad the m-tile (m % 32 != 0) and a padded odd block count (d = 96, 160)."""
+    import ctypes
+
+    rng = np.random.default_rng(m * 3 + d + prec)
+    x = to_dev(torch, (rng.standard_normal(m * d) * 3 + 0.7).astype(np.float32), (m, d))
+    g = to_dev(torch, rng.uniform(0.5, 1.5, d).astype(np.float32), (d,))
+    be = to_dev(torch, rng.uniform(-0.2, 0.2, d).astype(np.float32), (d,))
+    L = wq4.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    p = lambda a: ctypes.c_void_p(a.data_ptr())  # noqa: E731
+    atb = L.wq4_atiled_bytes(m, d, prec)
+    got = torch.full((atb,), 0x5A, dtype=torch.uint8, device="cuda:0")  # poisoned: every byte must be written
+    wq4.check(L.wq4_layernorm(p(x), p(g), p(be), m, d, prec, p(got), None, st))
+    y = torch.zeros((m, d), device="cuda:0")
+    wq4.check(L.wq4_layernorm(p(x), p(g), p(be), m, d, prec, None, p(y), st))
+    want = torch.zeros((atb,), dtype=torch.uint8, device="cuda:0")
+    wq4.check(L.wq4_tile_activations(p(y), m, d, d, prec, p(want), atb, st))
+    torch.cuda.synchronize()
+    ns = 2 if prec == 0 else 1
+    kbp = ((d // 32 + 1) // 2) * 2
+    nmt, kb = -(-m // 32), -(-d // 32)  # m-tiles and Q4 blocks the LayerNorm writes
+    gb = got.cpu().numpy().reshape(-1, kbp, 2, ns, 1024)[:nmt, :kb]
+    wb = want.cpu().numpy().reshape(-1, kbp, 2, ns, 1024)[:nmt, :kb]
+    assert np.array_equal(gb, wb)
+
+
 # ------------------------------------------- f16 weights (BASELINE config 5) --
 @pytest.mark.parametrize("policy", [1, 2, 3])
 @pytest.mark.parametrize("m,n,k", [(1, 1280, 1280), (32, 5120, 1280), (100, 1280, 5120), (1500, 1280, 1280),
