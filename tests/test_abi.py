@@ -7,6 +7,7 @@ runs before any device work, so its error behaviour is testable on the CPU.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -148,3 +149,38 @@ def test_every_whisper_header_function_is_exported():
     L = whisper_amd.lib()
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
+
+
+def test_decode_group_rows():
+    """wa_decode_group_rows: the clips of the largest decode group (the row
+    count of every captured decode-step launch and of bench.py's probe): one
+    group below 16 clips, two from 16 on (wa_model.cpp decode_groups)."""
+    import whisper_amd
+
+    assert whisper_amd.decode_group_rows(0) == 0
+    for n in range(1, 65):
+        want = n if n < 16 else (n + 1) // 2
+        assert whisper_amd.decode_group_rows(n) == want, n
+
+
+def test_bench_in_graph_lookup(tmp_path, monkeypatch):
+    """bench.in_graph_xattn sums the three cross-attention kernels at the
+    group's grids from profiles/xattn_in_graph.json, only for the same
+    workload."""
+    import json
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    wl = {"variant": "large_v3", "weights": "q4_0", "precision": "f16x2", "clips": 32}
+    (tmp_path / "profiles").mkdir()
+    rows = [{"kernel": "xattn_q_mfma_kernel", "grid": [2560, 20, 1], "avg_us": 5.5},
+            {"kernel": "xattn_main_kernel", "grid": [4096, 16, 1], "avg_us": 38.0},
+            {"kernel": "xattn_main_kernel", "grid": [4096, 32, 1], "avg_us": 48.0},
+            {"kernel": "xattn_out_kernel", "grid": [10240, 4, 1], "avg_us": 12.5}]
+    (tmp_path / "profiles" / "xattn_in_graph.json").write_text(json.dumps({"workload": wl, "kernels": rows}))
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    assert bench.in_graph_xattn(16, 20, 1280, wl) == 5.5 + 38.0 + 12.5
+    assert bench.in_graph_xattn(16, 20, 1280, dict(wl, clips=16)) is None
+    assert bench.in_graph_xattn(8, 20, 1280, wl) is None  # no trace at that grid
