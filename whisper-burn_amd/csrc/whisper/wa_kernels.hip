@@ -844,35 +844,44 @@ __device__ __forceinline__ void pick_from_lds(const float* lg, int B, int V, flo
 }
 
 constexpr int kLg2Chunk = 128;
-constexpr int kLg2Ld = kLg2Chunk + 8;  // halves
+// 16-row groups of the fragment-tiled table (V padded to 128-row workgroups)
+__host__ __device__ inline int64_t emb_groups16(int V) { return (int64_t)(V + 127) / 128 * 8; }
 
 // Tied-embedding logits of the decode step on f16 MFMA, fused with the greedy
 // pick: the embedding as exact-to-2^-22 f16 pairs E = hi + lo in a
 // fragment-tiled table (launch_emb_tiled: a lane's fragment is 8 dims of one
 // of 16 rows, one load instruction reads 1 KiB contiguous), the hidden rows
-// split likewise; three 16x16x32 f16 MFMAs per product (hi*hi + lo*hi +
-// hi*lo), f32 accumulation.  Wave = 32 vocabulary rows as two 16-row m-tiles,
-// the 32 clips as two n-tiles.  trace_out (diagnostics, null in the product
-// graph): the logits of trace_ids[clip][step + 1][0..trace_k) are written to
-// the same slots of trace_out, as the pick sees them (EOT already masked).
+// as the A-tiled f16-pair operand the final LayerNorm writes (wq4_layernorm,
+// the same split as the GEMMs); three 16x16x32 f16 MFMAs per product
+// (hi*hi + lo*hi + hi*lo), f32 accumulation.  Wave = 32 vocabulary rows as
+// two 16-row m-tiles, the 32 clips as two n-tiles.  Per 128-dim chunk the
+// hidden fragments (32 rows x 128 dims, 8 or 16 KiB) come into an LDS double
+// buffer through registers one chunk ahead, beside the next chunk's table
+// fragments in registers: one barrier per chunk, no conversion.  trace_out
+// (diagnostics, null in the product graph): the logits of
+// trace_ids[clip][step + 1][0..trace_k) are written to the same slots of
+// trace_out, as the pick sees them (EOT already masked).
 template <int NS>
 __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
-    const float* __restrict__ hid, int B, int D, long ldh, const _Float16* __restrict__ emb2, int V, int min_tokens,
+    const _Float16* __restrict__ htiled, int B, int D, const _Float16* __restrict__ emb2, int V, int min_tokens,
     const DecodeState* __restrict__ state, float* __restrict__ pval, int* __restrict__ pidx, int* __restrict__ counter,
     int* __restrict__ out_tok, const int* __restrict__ trace_ids, float* __restrict__ trace_out, int trace_s1,
     int trace_k) {
-  __shared__ __attribute__((aligned(16))) _Float16 hsh[NS][32 * kLg2Ld];
-  __shared__ __attribute__((aligned(16))) float lg[32 * kLgPickLd];
-  __shared__ int ticket;
+  constexpr int KS = kLg2Chunk / 32;             // Q4-block-sized k-steps per chunk
+  constexpr int HCH = KS * 2 * NS * 1024;        // bytes of hidden fragments per chunk
+  static_assert(HCH % (256 * 16) == 0, "whole glds rounds");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * HCH + 32 * kLgPickLd * 4 + 16];
+  float* lg = reinterpret_cast<float*>(smem + 2 * HCH);
+  int* ticket = reinterpret_cast<int*>(smem + 2 * HCH + 32 * kLgPickLd * 4);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, lq = lane >> 4;
   const int v0 = blockIdx.x * 128 + wave * 32;
-  // fragment-tiled table (launch_emb_tiled): this wave's two 16-row groups
-  const _Float16* er[2];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt) er[mt] = emb2 + (size_t)(v0 / 16 + mt) * (D / 32) * NS * 512 + lane * 8;
-  const int nch = (D + kLg2Chunk - 1) / kLg2Chunk;
-  constexpr int KS = kLg2Chunk / 32;
+  // chunk-major table (launch_emb_tiled): this wave's two 16-row groups are
+  // 2 KS NS KiB contiguous per chunk, and a chunk of the whole table is one
+  // contiguous stretch (every wave streams the same region at once)
+  const int nch = D / kLg2Chunk;
+  const size_t chunk_halves = (size_t)emb_groups16(V) * KS * NS * 512;
+  const _Float16* er = emb2 + (size_t)(v0 / 16) * KS * NS * 512 + lane * 8;
   floatx4 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -886,80 +895,68 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
         for (int p = 0; p < NS; ++p)  // D % kLg2Chunk == 0 (launcher): always in range
-          e[mt][ks][p] = *reinterpret_cast<const half8*>(er[mt] + ((size_t)(kc / 32 + ks) * NS + p) * 512);
+          e[mt][ks][p] = *reinterpret_cast<const half8*>(er + (kc / kLg2Chunk) * chunk_halves +
+                                                          ((mt * KS + ks) * NS + p) * 512);
   };
-  // the hidden rows of a chunk (f32, thread: row e / 32, 4 dims) travel one
-  // chunk ahead in registers too, so no chunk waits on a dependent load
-  constexpr int HPT = 32 * kLg2Chunk / 4 / 256;  // float4s per thread per chunk
-  floatx4 hc[HPT], hn[HPT];
-  // branch-free (clamped address, select after the load): the loads of a
-  // chunk form one straight-line group, so the compiler's vmcnt waits before
-  // the next chunk's use can leave the prefetched chunk in flight
-  auto load_h = [&](floatx4 (&hv)[HPT], int kc) {
+  // the hidden fragments of chunk c: A-tiled m-tile 0, blocks 4c .. 4c + 3
+  // (kk, plane, lane: 1 KiB each, contiguous), staged through registers into
+  // LDS buffer c & 1 lane-linear.  Not global_load_lds: while an LDS DMA is in
+  // flight hipcc waits vmcnt(0) at the first use of any ordinary load result
+  // (cdna_hip_programming.md "Pipelining across barriers"), which would drain
+  // the next chunk's table loads at the first MFMA of every chunk.
+  constexpr int HPT = HCH / (256 * 16);  // 16-B pieces per thread per chunk
+  half8 hr[HPT];
+  auto load_h = [&](int c) {
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(htiled) + (size_t)c * HCH;
 #pragma unroll
-    for (int i = 0; i < HPT; ++i) {
-      const int e = tid + 256 * i;
-      const int row = e / (kLg2Chunk / 4), k4 = (e % (kLg2Chunk / 4)) * 4;
-      const bool ok = row < B && kc + k4 < D;
-      const floatx4 v = *reinterpret_cast<const floatx4*>(hid + (size_t)(row < B ? row : 0) * ldh +
-                                                          (kc + k4 < D ? kc + k4 : 0));
-      hv[i] = ok ? v : floatx4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int i = 0; i < HPT; ++i) hr[i] = *reinterpret_cast<const half8*>(src + (i * 256 + tid) * 16);
   };
+  auto store_h = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < HPT; ++i) *reinterpret_cast<half8*>(smem + (c & 1) * HCH + (i * 256 + tid) * 16) = hr[i];
+  };
+  load_h(0);
   load_e(ec, 0);
-  load_h(hc, 0);
+  store_h(0);
+  __syncthreads();
   for (int c = 0; c < nch; ++c) {
-    const int kc = c * kLg2Chunk;
-    {  // the last chunk re-loads itself: no conditional load group
-      const int kn = c + 1 < nch ? kc + kLg2Chunk : kc;
-      load_e(en, kn);
-      load_h(hn, kn);
-    }
-    __syncthreads();
+    // hidden c + 1 first (its wait after the MFMAs then leaves the table loads
+    // in flight), the next chunk's table second
+    if (c + 1 < nch) load_h(c + 1);
+    load_e(en, c + 1 < nch ? (c + 1) * kLg2Chunk : c * kLg2Chunk);  // the last chunk re-loads itself
+    // keep the loads here: left to itself the scheduler sinks them below the
+    // MFMAs (fewer live registers), and every chunk then waits a full latency
+    __builtin_amdgcn_sched_barrier(0);
+    const uint8_t* hb = smem + (c & 1) * HCH;
 #pragma unroll
-    for (int i = 0; i < HPT; ++i) {  // (row, 4 dims) -> f16 pairs
-      const int e = tid + 256 * i;
-      const int row = e / (kLg2Chunk / 4), k4 = (e % (kLg2Chunk / 4)) * 4;
-      ea_half4 hi, lo;
+    for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        _Float16 a, b;
-        wq4::split_act(hc[i][j], a, b);
-        hi[j] = a;
-        lo[j] = b;
-      }
-      *reinterpret_cast<ea_half4*>(&hsh[0][row * kLg2Ld + k4]) = hi;
-      if constexpr (NS == 2) *reinterpret_cast<ea_half4*>(&hsh[NS - 1][row * kLg2Ld + k4]) = lo;
-    }
-    __syncthreads();
+      for (int nt = 0; nt < 2; ++nt) {
+        // B: clip 16 nt + l16, dims 32 ks + 8 lq .. + 7 = fragment (ks, kk = lq >> 1),
+        // lane' = clip + 32 (lq & 1)
+        const int off = ((ks * 2 + (lq >> 1)) * NS) * 1024 + (16 * nt + l16 + 32 * (lq & 1)) * 16;
+        const half8 bh = *reinterpret_cast<const half8*>(hb + off);
+        half8 bl;
+        if constexpr (NS == 2) bl = *reinterpret_cast<const half8*>(hb + off + 1024);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {  // D % kLg2Chunk == 0 (launcher): no partial chunk
-      {
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const int off = (16 * nt + l16) * kLg2Ld + 32 * ks + 8 * lq;
-          const half8 bh = *reinterpret_cast<const half8*>(&hsh[0][off]);
-          half8 bl;
-          if constexpr (NS == 2) bl = *reinterpret_cast<const half8*>(&hsh[1][off]);
-#pragma unroll
-          for (int mt = 0; mt < 2; ++mt) {
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ec[mt][ks][0], bh, acc[mt][nt], 0, 0, 0);
-            if constexpr (NS == 2) {
-              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ec[mt][ks][1], bh, acc[mt][nt], 0, 0, 0);
-              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ec[mt][ks][0], bl, acc[mt][nt], 0, 0, 0);
-            }
+        for (int mt = 0; mt < 2; ++mt) {
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ec[mt][ks][0], bh, acc[mt][nt], 0, 0, 0);
+          if constexpr (NS == 2) {
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ec[mt][ks][1], bh, acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ec[mt][ks][0], bl, acc[mt][nt], 0, 0, 0);
           }
         }
       }
     }
+    // buffer (c + 1) & 1 was last read in chunk c - 1, before the previous barrier
+    if (c + 1 < nch) store_h(c + 1);
+    __syncthreads();  // no LDS DMA in flight: a bare s_barrier, the table loads survive it
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
         for (int p = 0; p < NS; ++p) ec[mt][ks][p] = en[mt][ks][p];
-#pragma unroll
-    for (int i = 0; i < HPT; ++i) hc[i] = hn[i];
   }
   // acc[mt][nt]: lane holds clip 16 nt + l16, vocab v0 + 16 mt + 4 lq + j
   const int suppress = state->step + 1 < min_tokens;
@@ -986,21 +983,26 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
         if (id >= 0 && id < 128) trace_out[o] = lg[b * kLgPickLd + id];
       }
   }
-  pick_from_lds(lg, B, V, pval, pidx, counter, out_tok, &ticket);
+  pick_from_lds(lg, B, V, pval, pidx, counter, out_tok, ticket);
 }
 
 int logits_argmax_groups(int V) { return (V + 127) / 128; }
 
-// f32 rows -> fragment-tiled f16 planes; thread = (group, step, lane): 8 values
+// f32 rows -> fragment-tiled f16 planes, chunk-major: fragment
+// f = (chunk * groups + g) * KS + ks holds rows 16 g .. + 15, dims
+// 128 chunk + 32 ks + 8 (lane >> 4) .. + 7; thread = (fragment, lane): 8 values
 template <int NS>
 __global__ __launch_bounds__(256) void emb_tiled_kernel(const float* __restrict__ x, int V, int D, int64_t nfrag,
                                                         _Float16* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= nfrag * 64) return;
   const int lane = (int)(i & 63);
-  const int64_t f = i >> 6;  // g * (D / 32) + s
-  const int64_t g = f / (D / 32);
-  const int s = (int)(f - g * (D / 32));
+  constexpr int KS = kLg2Chunk / 32;
+  const int64_t f = i >> 6;
+  const int64_t groups = emb_groups16(V);
+  const int64_t cg = f / KS;  // chunk * groups + g
+  const int64_t chunk = cg / groups, g = cg - chunk * groups;
+  const int s = (int)(chunk * KS + (f - cg * KS));
   const int64_t v = g * 16 + (lane & 15);
   const int k = s * 32 + 8 * (lane >> 4);
   half8 hi, lo;
@@ -1029,17 +1031,17 @@ hipError_t launch_emb_tiled(const float* emb, int V, int D, int ns, _Float16* ou
   return hipGetLastError();
 }
 
-hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const _Float16* emb2, int ns, int V,
+hipError_t launch_logits_argmax(const _Float16* htiled, int B, int D, const _Float16* emb2, int ns, int V,
                                 int min_tokens, const DecodeState* state, float* pval, int* pidx, int* counter,
                                 int* out_tok, const int* trace_ids, float* trace_out, int trace_s1, int trace_k,
                                 hipStream_t st) {
-  if (B < 1 || B > 32 || !emb_tiled_supported(D) || !state || !emb2) return hipErrorInvalidValue;
+  if (B < 1 || B > 32 || !emb_tiled_supported(D) || !state || !emb2 || !htiled) return hipErrorInvalidValue;
   const dim3 grid(logits_argmax_groups(V));
   if (ns == 2)
-    hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<2>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens,
+    hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<2>, grid, dim3(256), 0, st, htiled, B, D, emb2, V, min_tokens,
                        state, pval, pidx, counter, out_tok, trace_ids, trace_out, trace_s1, trace_k);
   else
-    hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<1>, grid, dim3(256), 0, st, h, B, D, ldh, emb2, V, min_tokens,
+    hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<1>, grid, dim3(256), 0, st, htiled, B, D, emb2, V, min_tokens,
                        state, pval, pidx, counter, out_tok, trace_ids, trace_out, trace_s1, trace_k);
   return hipGetLastError();
 }

@@ -87,10 +87,12 @@ hipError_t launch_argmax(const float* logits, int B, int V, int lo, int hi, int 
 // D % 8 == 0; pval / pidx: 32 * logits_argmax_groups(V) scratch each,
 // counter: one int zeroed once (re-armed by the kernel).
 int logits_argmax_groups(int V);
-// emb2: the f16-pair table, fragment-tiled (launch_emb_tiled); D % 128 == 0.
+// htiled: the B hidden rows as the A-tiled operand (wq4 layout, m-tile 0,
+// ns planes -- what wq4_layernorm writes with at_out); emb2: the f16-pair
+// table, fragment-tiled (launch_emb_tiled); D % 128 == 0.
 // trace_ids / trace_out (diagnostics; null in the product): [B][trace_s1]
 // [trace_k] -- the logits of the listed ids at slot state->step + 1.
-hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const _Float16* emb2, int ns, int V,
+hipError_t launch_logits_argmax(const _Float16* htiled, int B, int D, const _Float16* emb2, int ns, int V,
                                 int min_tokens, const DecodeState* state, float* pval, int* pidx, int* counter,
                                 int* out_tok, const int* trace_ids, float* trace_out, int trace_s1, int trace_k,
                                 hipStream_t st);
@@ -98,11 +100,13 @@ hipError_t launch_logits_argmax(const float* h, int B, int D, long ldh, const _F
 bool emb_tiled_supported(int D);
 // Rows of the fragment-tiled table (V padded to the kernel's 128-row groups).
 int64_t emb_tiled_rows(int V);
-// f32 [V][D] -> fragment-tiled f16 planes: per 16-row group g, 32-column
-// step s and plane p, the 16x16x32 MFMA operand of 64 lanes x 8 halves is
-// 1 KiB contiguous at ((g * D / 32 + s) * ns + p) KiB (lane = 16 (k / 8 % 4)
-// + row % 16), rows >= V zero -- every load instruction of the logits
-// kernel reads 1 KiB contiguous.  out: emb_tiled_rows(V) * ns * D halves.
+// f32 [V][D] -> fragment-tiled f16 planes, chunk-major: per 128-column
+// chunk c, 16-row group g (G = emb_tiled_rows(V) / 16 of them), 32-column
+// step ks < 4 and plane p, the 16x16x32 MFMA operand of 64 lanes x 8 halves
+// is 1 KiB contiguous at (((c * G + g) * 4 + ks) * ns + p) KiB (lane =
+// 16 (k / 8 % 4) + row % 16), rows >= V zero -- every load instruction of
+// the logits kernel reads 1 KiB contiguous and one chunk of the whole table
+// is one contiguous stretch.  out: emb_tiled_rows(V) * ns * D halves.
 hipError_t launch_emb_tiled(const float* emb, int V, int D, int ns, _Float16* out, hipStream_t st);
 
 // Greedy-loop bookkeeping at the top of each step (whisper.rs:104-115):

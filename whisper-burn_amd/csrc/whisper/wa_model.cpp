@@ -176,7 +176,8 @@ struct DecGroup {
   float* xattn_part;  // cross-attention split partials (Z, max, sum)
   _Float16* atd_ln;   // LayerNorm fold: A-tiled x * gamma of the next LayerNorm
   float* ln_stats;    //                 its per (row, 32-column tile) mean / M2
-  float* lg_val;      // fused logits + argmax: per-workgroup candidates [32][groups]
+  _Float16* hid_t;    // fused logits + argmax: the final LN, A-tiled (m-tile 0)
+  float* lg_val;      //                        per-workgroup candidates [32][groups]
   int *lg_idx, *lg_ctr;
   wa::DecodeState* state;
   int* host_ndone = nullptr;  // pinned ring
@@ -639,6 +640,7 @@ wq4_status alloc_activations(wa_model* m) {
     g.xqt = d.alloc<_Float16>((size_t)rdec * m->ns * HP * Dt);
     g.atd_ln = tiled(rdec, Dt);
     g.ln_stats = f32(rdec * (Dt / 16) * 2);  // per 16-column tile (the decode-step GEMM)
+    g.hid_t = tiled(rdec, Dt);
     g.lg_val = f32((int64_t)32 * wa::logits_argmax_groups(c.n_vocab));
     g.lg_idx = d.alloc<int>((size_t)32 * wa::logits_argmax_groups(c.n_vocab));
     g.lg_ctr = d.alloc<int>(1);
@@ -646,9 +648,10 @@ wq4_status alloc_activations(wa_model* m) {
     for (void* p : {(void*)g.xd, (void*)g.qkvd, (void*)g.qd, (void*)g.hid, (void*)g.logits, (void*)g.atd_dec,
                     (void*)g.atf_dec, (void*)g.prompt_tok, (void*)g.next_tok, (void*)g.tokens, (void*)g.ntok,
                     (void*)g.done, (void*)g.state, (void*)g.xattn_part, (void*)g.xqt, (void*)g.lg_val,
-                    (void*)g.lg_idx, (void*)g.lg_ctr, (void*)g.atd_ln, (void*)g.ln_stats})
+                    (void*)g.lg_idx, (void*)g.lg_ctr, (void*)g.atd_ln, (void*)g.ln_stats, (void*)g.hid_t})
       if (!p) return fail(WQ4_ENOMEM, "decode-group allocation failed");
     WA_HIP(hipMemset(g.atd_ln, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
+    WA_HIP(hipMemset(g.hid_t, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));  // padded clips stay 0
     WA_HIP(hipMemset(g.lg_ctr, 0, sizeof(int)));
     WA_HIP(hipMemset(g.xqt, 0, (size_t)rdec * m->ns * HP * Dt * 2));  // padded heads stay 0
     WA_HIP(hipMemset(g.atd_dec, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
@@ -855,14 +858,17 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
   }
   // final LN (decoder.rs:286 / 340) and tied-embedding logits of the last
   // position of every clip (decoder.rs:289-292, 342-343)
-  WA_WQ4(wq4_layernorm(g.xd, m->dln_w, m->dln_b, rows, D, WQ4_PREC_F16X2, nullptr, g.hid, st));
   if (fused_pick(g, Tq, state)) {  // decode step: logits + greedy pick in one kernel, into next_tok
+    // the final LN writes the pick's operand directly (A-tiled, the
+    // embedding planes' precision)
+    WA_WQ4(wq4_layernorm(g.xd, m->dln_w, m->dln_b, rows, D, m->prec, g.hid_t, nullptr, st));
     const size_t tofs = (size_t)g.b0 * m->trace_s1 * m->trace_k;
-    WA_HIP(wa::launch_logits_argmax(g.hid, B, D, D, m->tok_emb2, m->ns, c.n_vocab, kMinTokens, state, g.lg_val,
+    WA_HIP(wa::launch_logits_argmax(g.hid_t, B, D, m->tok_emb2, m->ns, c.n_vocab, kMinTokens, state, g.lg_val,
                                     g.lg_idx, g.lg_ctr, g.next_tok, m->trace_out ? m->trace_ids + tofs : nullptr,
                                     m->trace_out ? m->trace_out + tofs : nullptr, m->trace_s1, m->trace_k, st));
     return WQ4_OK;
   }
+  WA_WQ4(wq4_layernorm(g.xd, m->dln_w, m->dln_b, rows, D, WQ4_PREC_F16X2, nullptr, g.hid, st));
   WA_HIP(wa::launch_logits(g.hid + (size_t)(Tq - 1) * D, B, D, (int64_t)Tq * D, m->tok_emb, c.n_vocab, g.logits,
                            st));
   return WQ4_OK;
@@ -1454,10 +1460,14 @@ wq4_status wa_logits_argmax_check(int device, const float* hid_dev, const float*
   auto* pval = d.alloc<float>((size_t)32 * ng);
   auto* pidx = d.alloc<int>((size_t)32 * ng);
   auto* ctr = d.alloc<int>(1);
+  const size_t tb = wq4_atiled_bytes(n_clips, D, prec);
+  auto* ht = d.alloc<_Float16>(tb / 2);
   int* ids = nullptr;
   if (logits_dev) ids = d.alloc<int>((size_t)n_clips * 2 * V);
-  if (!emb2 || !st || !pval || !pidx || !ctr || (logits_dev && !ids)) return fail(WQ4_ENOMEM, "allocation failed");
+  if (!emb2 || !st || !pval || !pidx || !ctr || !ht || (logits_dev && !ids))
+    return fail(WQ4_ENOMEM, "allocation failed");
   WA_HIP(wa::launch_emb_tiled(emb_dev, V, D, ns, emb2, nullptr));
+  WA_WQ4(wq4_tile_activations(hid_dev, n_clips, D, D, prec, ht, tb, nullptr));
   // A trace writes slot state->step + 1 of [clip][2][V] (every id listed at
   // slot 1): the state's step is then 0 and the EOT suppression of `step`
   // (step + 1 < 3, whisper.rs:120-122) is passed through min_tokens instead.
@@ -1474,7 +1484,7 @@ wq4_status wa_logits_argmax_check(int device, const float* hid_dev, const float*
     tr = d.alloc<float>((size_t)n_clips * 2 * V);
     if (!tr) return fail(WQ4_ENOMEM, "allocation failed");
   }
-  WA_HIP(wa::launch_logits_argmax(hid_dev, n_clips, D, D, emb2, ns, V, min_tokens, st, pval, pidx, ctr, tok_dev,
+  WA_HIP(wa::launch_logits_argmax(ht, n_clips, D, emb2, ns, V, min_tokens, st, pval, pidx, ctr, tok_dev,
                                   ids, tr, 2, V, nullptr));
   if (logits_dev)
     for (int b = 0; b < n_clips; ++b)
