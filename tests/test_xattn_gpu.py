@@ -92,6 +92,36 @@ def test_xattn_f16_precision(torch):
     assert np.abs(got - ref).max() / np.abs(ref).max() <= 5e-3
 
 
+@pytest.mark.parametrize("B,Tq,T,H", [
+    (1, 1, 1500, 20),   # Large-V3, one clip (BASELINE config 3)
+    (3, 1, 1500, 20),
+    (1, 4, 1500, 20),   # one clip's prompt rows
+    (8, 1, 1500, 20),   # the largest split-phase batch
+    (2, 1, 1500, 16),   # Medium (one head tile)
+    (2, 1, 200, 6),     # test configuration (4 waves per slice)
+    (1, 1, 37, 20),     # a ragged last sub-chunk, one sub-chunk per split
+])
+def test_xattn_small_rows_bit_identical(torch, monkeypatch, B, Tq, T, H):
+    """The split-phase path for few query rows (scores / softmax / z launches,
+    wa_xattn.hip) reproduces the fused kernel's partials bit for bit, so the
+    output -- and a clip's tokens -- do not depend on which path its batch
+    size selects; both are within the f16x2 tolerance of the reference."""
+    monkeypatch.setenv("WA_XATTN_SMALL_ROWS", "0")
+    fused, ref = run_case(torch, B, Tq, T, H, seed=11)
+    monkeypatch.setenv("WA_XATTN_SMALL_ROWS", "8")
+    split, _ = run_case(torch, B, Tq, T, H, seed=11)
+    assert np.array_equal(fused, split), np.abs(fused - split).max()
+    assert np.abs(split - ref).max() / np.abs(ref).max() <= 2e-5
+
+
+def test_xattn_small_rows_f16_precision(torch, monkeypatch):
+    monkeypatch.setenv("WA_XATTN_SMALL_ROWS", "0")
+    fused, _ = run_case(torch, 2, 1, 1500, 20, prec=wq4.PREC_F16, seed=12)
+    monkeypatch.setenv("WA_XATTN_SMALL_ROWS", "8")
+    split, _ = run_case(torch, 2, 1, 1500, 20, prec=wq4.PREC_F16, seed=12)
+    assert np.array_equal(fused, split)
+
+
 def test_xattn_rows_independent(torch):
     """Each query row's result is independent of the batch it runs in."""
     import whisper_amd

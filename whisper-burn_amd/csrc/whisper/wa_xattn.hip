@@ -63,6 +63,16 @@ constexpr float kZnScale = 32.0f, kWvScale = 4096.0f, kOutInv = 1.0f / (32.0f * 
 // the isolated 16-clip launch faster (50.5 us vs 55.7 at 12) but the decode
 // slower (926 / 1073 ms vs 873): more workgroups crowd out the other group.
 constexpr int kXattnSplits = WA_XATTN_SPLITS;
+// Timing attribution builds of tools/xattn_micro.hip only (wrong results):
+// 1 = no encoder fetch after the first sub-chunk, 2 = no Z phase, 3 = no
+// score MFMAs, 4 = no softmax, 5 = never rescale Z, 6 = no barrier after the
+// score partials, 7 = no barrier after the softmax, 8 = softmax computed but
+// P stored as zeros, 9 = no softmax, P = 1, 10 = no sub-chunk loop (fixed
+// cost: qt loads, LDS init, partial stores).  0 (the product)
+// compiles none of them.
+#ifndef WA_XATTN_DIAG
+#define WA_XATTN_DIAG 0
+#endif
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -218,7 +228,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   const int c0 = w * CW;
   const int ts = s * CH * kTc;
   const int te = min(T, ts + CH * kTc);
-  const int nch = te > ts ? (te - ts + kTc - 1) / kTc : 0;
+  const int nch = WA_XATTN_DIAG == 10 ? 0 : te > ts ? (te - ts + kTc - 1) / kTc : 0;
 
   // qt operands (B of the score MFMA: k = column, n = head): head tile 0 in
   // registers; for H in (16, 20] the 4 heads of tile 1 from LDS (registers of
@@ -240,7 +250,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     }
   }
   // rows of P past the score tiles stay 0, their alpha 1
-  for (int i = tid; i < NS * 32 * (kTc + 8); i += kThreads) (&sp[0][0][0])[i] = (_Float16)0.0f;
+  for (int i = tid; i < NS * 32 * (kTc + 8); i += kThreads) (&sp[0][0][0])[i] = (_Float16)(WA_XATTN_DIAG == 9 ? 1.0f : 0.0f);
   if (tid < 32) salpha[tid] = 1.0f;
   if (tid < 2) srescale[tid] = 0;
   if (tid < 8) szero[tid] = (_Float16)0.0f;
@@ -315,7 +325,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
 #pragma unroll
     for (int ht = 0; ht < HT; ++ht) sacc[ht] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
+    for (int ks = 0; ks < (WA_XATTN_DIAG == 3 ? 0 : KS); ++ks) {
       half8 a[NS];
 #pragma unroll
       for (int p = 0; p < NS; ++p) a[p] = afrag(ks, p);
@@ -346,7 +356,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
 #pragma unroll
     for (int e = 0; e < SMX; ++e) {
       const int idx = tid + e * kThreads;
-      if (idx < HT * 256) {
+      if (idx < HT * 256 && WA_XATTN_DIAG != 4 && WA_XATTN_DIAG != 9) {
         const int ht = idx >> 8, hh = (idx >> 4) & 15, t = idx & 15;
         const int h = ht * 16 + hh;
         float sv = 0.0f;
@@ -366,13 +376,14 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
         M[e] = mn;
         _Float16 phi, plo;
         split_f16(p * kPScale, phi, plo);  // p * 2^15: the lo half stays a normal f16 (undone at the store)
+        if (WA_XATTN_DIAG == 8) phi = plo = (_Float16)0.0f;
         sp[0][h][t] = phi;
         if (NS == 2) sp[1][h][t] = plo;
         if (t == 0) salpha[h] = alpha;
-        if (alpha != 1.0f) srescale[chi & 1] = 1;  // benign race: every writer stores 1
+        if (alpha != 1.0f && WA_XATTN_DIAG != 5) srescale[chi & 1] = 1;  // benign race: every writer stores 1
       }
     }
-    __syncthreads();
+    if (WA_XATTN_DIAG != 7) __syncthreads();
     // alpha == 1 for every head (no running maximum moved, the steady state)
     // makes the rescale a multiplication by 1: skipped, bit-identical
     const bool rescale = srescale[chi & 1] != 0;
@@ -391,7 +402,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
       }
     }
 #pragma unroll
-    for (int ct = 0; ct < KS; ++ct) {
+    for (int ct = 0; ct < (WA_XATTN_DIAG == 2 ? 0 : KS); ++ct) {
       half8 eb[NS];
 #pragma unroll
       for (int p = 0; p < NS; ++p) {
@@ -412,11 +423,11 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   auto step = [&](u32x4v (&buf)[NLD], int chi) {
     const int t0 = ts + chi * kTc;
     write_se(buf);
-    if (chi + PF < nch) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
+    if (chi + PF < nch && WA_XATTN_DIAG != 1) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
     scores([&](int ks, int p) {
       return *reinterpret_cast<const half8*>(&se[l16 * RS + p * D + c0 + ks * 32 + 8 * lq_sw]);
     });
-    __syncthreads();  // every wave's score partials in red
+    if (WA_XATTN_DIAG != 6) __syncthreads();  // every wave's score partials in red
     tail(chi, t0);
   };
   u32x4v pre0[NLD];
@@ -679,6 +690,286 @@ __global__ __launch_bounds__(256) void untile_kernel(const _Float16* __restrict_
   out[i] = v * wq4::kActScaleInv;
 }
 
+// ------------------------------------------- few query rows: split phases --
+// With R query rows the fused xattn_main_kernel runs S * R workgroups (8 at
+// one clip), each walking its CH sub-chunks in series (2.7 us each at 16
+// clips).  For R <= xattn_small_rows() the same arithmetic runs as three
+// launches that spread over sub-chunks and columns instead:
+//   scores   one workgroup per (row, sub-chunk): the fused kernel's score
+//            MFMA sequence per wave column slice, its wave-order partial sum;
+//   softmax  one workgroup per (row, split): the fused kernel's online softmax
+//            step by step (same lanes, DPP reductions, rescale flag);
+//   z        one wave per (row, split, 32-column tile): the fused kernel's
+//            rescale + three MFMAs per sub-chunk on that tile.
+// Every partial (Z, max, sum) therefore has the fused path's bits, so a
+// clip's tokens do not depend on the batch (test_xattn_small_rows_bit_identical).
+constexpr int kSmallMaxCH = 12;   // sub-chunks per split the softmax/z kernels preload (T <= 1536 at 8 splits)
+constexpr int kSmallRowsMax = 8;  // scratch is sized for up to this many rows
+
+template <int D, int HT, int NS, int NW>
+__global__ __launch_bounds__(64 * NW) void xattn_scores_kernel(const _Float16* __restrict__ qt,
+                                                               const _Float16* __restrict__ enc, int Tq, int T,
+                                                               int NG, float* __restrict__ sbuf) {
+  constexpr int CW = D / NW, KS = CW / 32, HP = HT * 16, ROW = NS * D;
+  __shared__ __attribute__((aligned(16))) float red[NW][HT][16][20];
+  const int g = blockIdx.x, r = blockIdx.y;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, l16 = l & 15, lq = l >> 4;
+  const int c0 = w * CW, f = g * kTc + l16;
+  const _Float16* E = enc + (size_t)(r / Tq) * T * ROW;
+  // A = this wave's column slice of the sub-chunk's frames (frames >= T are
+  // zeros, as the fused kernel's buffer loads give); B = qt, the second head
+  // tile's padding lanes zero
+  half8 a[KS][NS];
+  const int fc = f < T ? f : T - 1;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int p = 0; p < NS; ++p)
+      a[ks][p] = *reinterpret_cast<const half8*>(E + (size_t)fc * ROW + p * D + c0 + ks * 32 + 8 * lq);
+  if (f >= T) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int p = 0; p < NS; ++p) a[ks][p] = half8{};
+  }
+  half8 qb[KS][HT][NS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int ht = 0; ht < HT; ++ht) {
+      // padding lanes of the second head tile read their group's real row
+      // (no extra bytes fetched) and are zeroed below
+      const int hr = (HT == 2 && ht == 1) ? 16 + (l16 & 3) : ht * 16 + l16;
+#pragma unroll
+      for (int p = 0; p < NS; ++p)
+        qb[ks][ht][p] = *reinterpret_cast<const half8*>(qt + (((size_t)r * NS + p) * HP + hr) * D + c0 + ks * 32 + 8 * lq);
+    }
+  __builtin_amdgcn_sched_barrier(0);  // every load above in flight before the first MFMA
+  floatx4 sacc[HT];
+#pragma unroll
+  for (int ht = 0; ht < HT; ++ht) sacc[ht] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int ht = 0; ht < HT; ++ht) {
+      const bool ok = !(HT == 2 && ht == 1) || l16 < 4;
+      half8 b[NS];
+#pragma unroll
+      for (int p = 0; p < NS; ++p) b[p] = ok ? qb[ks][ht][p] : half8{};
+      sacc[ht] = mfma16x32(a[ks][0], b[0], sacc[ht]);
+      if constexpr (NS == 2) {
+        sacc[ht] = mfma16x32(a[ks][1], b[0], sacc[ht]);
+        sacc[ht] = mfma16x32(a[ks][0], b[1], sacc[ht]);
+      }
+    }
+#pragma unroll
+  for (int ht = 0; ht < HT; ++ht) *reinterpret_cast<floatx4*>(&red[w][ht][l16][4 * lq]) = sacc[ht];
+  __syncthreads();
+  for (int idx = tid; idx < HT * 256; idx += 64 * NW) {
+    const int ht = idx >> 8, hh = (idx >> 4) & 15, t = idx & 15;
+    float sv = 0.0f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) sv += red[ww][ht][hh][t];
+    sbuf[(((size_t)r * NG + g) * HP + ht * 16 + hh) * 16 + t] = sv;
+  }
+}
+
+// pbuf [row][sub-chunk][NS][32 heads][16 frames] f16 (P * 2^15 split), abuf
+// [row][sub-chunk][32] alpha.  Every head's 16 lanes run on their own: no
+// barrier (the rescale flag is derived from the alphas by the z kernel).
+template <int HT, int NS, int NW>
+__global__ __launch_bounds__(64 * NW) void xattn_softmax_kernel(const float* __restrict__ sbuf, int T, int H, int S,
+                                                                int CH, int NG, _Float16* __restrict__ pbuf,
+                                                                float* __restrict__ abuf, float* __restrict__ mlpart) {
+  constexpr int kThreads = 64 * NW, HP = HT * 16;
+  constexpr int SMX = 512 / kThreads;  // entries (head 0..31, frame) per thread
+  const int s = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
+  const int ts = s * CH * kTc, te = min(T, ts + CH * kTc);
+  const int nch = te > ts ? (te - ts + kTc - 1) / kTc : 0;
+  float sv_all[kSmallMaxCH][SMX];
+#pragma unroll
+  for (int c = 0; c < kSmallMaxCH; ++c)
+#pragma unroll
+    for (int e = 0; e < SMX; ++e) {
+      const int idx = tid + e * kThreads, h = idx >> 4, t = idx & 15;
+      const int cc = c < nch ? c : 0, hc = h < HP ? h : 0;  // every load issued up front (no branch)
+      sv_all[c][e] = sbuf[(((size_t)r * NG + s * CH + cc) * HP + hc) * 16 + t];
+    }
+  float M[SMX], L[SMX];
+#pragma unroll
+  for (int e = 0; e < SMX; ++e) {
+    M[e] = -INFINITY;
+    L[e] = 0.0f;
+  }
+#pragma unroll
+  for (int chi = 0; chi < kSmallMaxCH; ++chi) {
+    if (chi >= nch) break;
+    const int t0 = ts + chi * kTc;
+    const size_t gi = (size_t)r * NG + s * CH + chi;
+#pragma unroll
+    for (int e = 0; e < SMX; ++e) {
+      const int idx = tid + e * kThreads, h = idx >> 4, t = idx & 15;
+      _Float16 phi = (_Float16)0.0f, plo = (_Float16)0.0f;
+      float alpha = 1.0f;
+      if (h < HP) {  // the fused kernel's softmax entry, verbatim
+        float sv = sv_all[chi][e];
+        const bool valid = h < H && t0 + t < te;
+        sv = valid ? sv : -INFINITY;
+        const float cm = wq4::max16(sv);
+        const float mn = fmaxf(M[e], cm);
+        float p = 0.0f;
+        if (mn != -INFINITY) {
+          alpha = __builtin_amdgcn_exp2f((M[e] - mn) * kSInv);
+          p = valid ? __builtin_amdgcn_exp2f((sv - mn) * kSInv) : 0.0f;
+        }
+        const float ps = wq4::sum16(p);
+        L[e] = L[e] * alpha + ps;
+        M[e] = mn;
+        split_f16(p * kPScale, phi, plo);
+      }
+      pbuf[((gi * NS + 0) * 32 + h) * 16 + t] = phi;
+      if (NS == 2) pbuf[((gi * NS + 1) * 32 + h) * 16 + t] = plo;
+      if (t == 0) abuf[gi * 32 + h] = alpha;
+    }
+  }
+  const size_t base = (size_t)r * S + s;
+#pragma unroll
+  for (int e = 0; e < SMX; ++e) {
+    const int idx = tid + e * kThreads, h = idx >> 4;
+    if ((idx & 15) == 0 && h < H && h < HP) {
+      mlpart[(base * H + h) * 2] = M[e] * kSInv;
+      mlpart[(base * H + h) * 2 + 1] = L[e];
+    }
+  }
+}
+
+// grid (S, D / 128, R), 4 waves: wave w owns columns cb .. cb + 31 of split s
+template <int D, int NS>
+__global__ __launch_bounds__(256) void xattn_z_kernel(const _Float16* __restrict__ enc,
+                                                      const _Float16* __restrict__ pbuf,
+                                                      const float* __restrict__ abuf,
+                                                      int Tq, int T, int H, int S, int CH, int NG,
+                                                      float* __restrict__ zpart) {
+  constexpr int ROW = NS * D, ZR = 32;  // staged plane: 16 frames x 32 columns, rows of 64 B
+  __shared__ __attribute__((aligned(16))) _Float16 sp[kSmallMaxCH][NS][32][kTc];
+  __shared__ float sal[kSmallMaxCH][32];
+  __shared__ int sfl[kSmallMaxCH];
+  __shared__ __attribute__((aligned(16))) _Float16 stg[4][NS][16 * ZR];
+  const int s = blockIdx.x, r = blockIdx.z, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int l32 = l & 31, lh = l >> 5;
+  const int cb = blockIdx.y * 128 + w * 32;
+  const int ts = s * CH * kTc, te = min(T, ts + CH * kTc);
+  const int nch = te > ts ? (te - ts + kTc - 1) / kTc : 0;
+  const size_t g0 = (size_t)r * NG + s * CH;
+  // this wave's enc pieces of every sub-chunk (lane: frame l >> 2, 8 columns
+  // 8 (l & 3)), frames past the split read as zeros
+  typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  const _Float16* E = enc + (size_t)(r / Tq) * T * ROW;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<_Float16*>(E + (size_t)ts * ROW), 0, nch > 0 ? (te - ts) * ROW * 2 : 0, 0x00020000);
+  u32x4v ev[kSmallMaxCH][NS];
+#pragma unroll
+  for (int c = 0; c < kSmallMaxCH; ++c)
+#pragma unroll
+    for (int p = 0; p < NS; ++p)  // unconditional: past the split's frames the buffer gives zeros
+        ev[c][p] = __builtin_amdgcn_raw_buffer_load_b128(
+            rs, (uint32_t)((((c * kTc + (l >> 2)) * ROW) + p * D + cb + 8 * (l & 3)) * 2), 0, 0);
+  // P and alpha of the split (shared by the 4 waves): every load issued
+  // before any is stored; the rescale flag of a sub-chunk = some alpha != 1
+  // (the fused kernel's srescale)
+  constexpr int NPV = kSmallMaxCH * NS * 32 * kTc / 8 / 256;  // half8 per thread
+  constexpr int NAV = (kSmallMaxCH * 32 + 255) / 256;
+  half8 pv[NPV];
+  float av[NAV];
+  const int npv = nch * NS * 32 * kTc / 8, nav = nch * 32;
+#pragma unroll
+  for (int u = 0; u < NPV; ++u) {
+    const int i = tid + 256 * u;
+    pv[u] = reinterpret_cast<const half8*>(pbuf + g0 * NS * 32 * kTc)[i < npv ? i : 0];
+  }
+#pragma unroll
+  for (int u = 0; u < NAV; ++u) {
+    const int i = tid + 256 * u;
+    av[u] = abuf[g0 * 32 + (i < nav ? i : 0)];
+  }
+  if (tid < kSmallMaxCH) sfl[tid] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < NPV; ++u) {
+    const int i = tid + 256 * u;
+    if (i < npv) reinterpret_cast<half8*>(&sp[0][0][0][0])[i] = pv[u];
+  }
+#pragma unroll
+  for (int u = 0; u < NAV; ++u) {
+    const int i = tid + 256 * u;
+    if (i < nav) {
+      (&sal[0][0])[i] = av[u];
+      if (av[u] != 1.0f) sfl[i >> 5] = 1;  // benign race: every writer stores 1
+    }
+  }
+  __syncthreads();
+  const int g = l >> 4, gi = l & 15;
+  const int trow = 8 * (g >> 1) + (gi >> 2), tcol = 16 * (g & 1) + 4 * (gi & 3);
+  floatx16 zacc;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) zacc[j] = 0.0f;
+#pragma unroll
+  for (int chi = 0; chi < kSmallMaxCH; ++chi) {
+    if (chi >= nch) continue;
+#pragma unroll
+    for (int p = 0; p < NS; ++p)
+      *reinterpret_cast<u32x4v*>(&stg[w][p][(l >> 2) * ZR + 8 * (l & 3)]) = ev[chi][p];
+    half8 pa[NS];
+#pragma unroll
+    for (int p = 0; p < NS; ++p) pa[p] = *reinterpret_cast<const half8*>(&sp[chi][p][l32][8 * lh]);
+    if (sfl[chi]) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) zacc[j] *= sal[chi][(j & 3) + 8 * (j >> 2) + 4 * lh];
+    }
+    half8 eb[NS];
+#pragma unroll
+    for (int p = 0; p < NS; ++p) {
+      const half4 x0 = lds_tr4(&stg[w][p][trow * ZR + tcol]);
+      const half4 x1 = lds_tr4(&stg[w][p][(trow + 4) * ZR + tcol]);
+      eb[p] = half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    }
+    zacc = mfma32x16(pa[0], eb[0], zacc);
+    if (NS == 2) {
+      zacc = mfma32x16(pa[1], eb[0], zacc);
+      zacc = mfma32x16(pa[0], eb[1], zacc);
+    }
+  }
+  const size_t base = (size_t)r * S + s;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int h = (j & 3) + 8 * (j >> 2) + 4 * lh;
+    if (h < H) zpart[(base * H + h) * D + cb + l32] = zacc[j] * kZInv;
+  }
+}
+
+template <int D, int HT, int NS>
+void launch_small(int R, int Tq, int T, int H, const XattnPlan& p, const _Float16* qt, const _Float16* enc,
+                  float* z, float* ml, float* scratch, hipStream_t st) {
+  constexpr int NW = (D / 8) % 32 == 0 ? 8 : 4;
+  const int NG = p.splits * p.ch;
+  float* sb = scratch;                                                       // R * NG * 32 * 16 floats
+  _Float16* pb = reinterpret_cast<_Float16*>(sb + (size_t)R * NG * 32 * 16);  // R * NG * 2 * 32 * 16 halves
+  float* ab = reinterpret_cast<float*>(pb + (size_t)R * NG * 2 * 32 * 16);    // R * NG * 32
+  hipLaunchKernelGGL((xattn_scores_kernel<D, HT, NS, NW>), dim3(NG, R), dim3(64 * NW), 0, st, qt, enc, Tq, T, NG, sb);
+  hipLaunchKernelGGL((xattn_softmax_kernel<HT, NS, NW>), dim3(p.splits, R), dim3(64 * NW), 0, st, sb, T, H,
+                     p.splits, p.ch, NG, pb, ab, ml);
+  hipLaunchKernelGGL((xattn_z_kernel<D, NS>), dim3(p.splits, D / 128, R), dim3(256), 0, st, enc, pb, ab, Tq, T,
+                     H, p.splits, p.ch, NG, z);
+}
+
+// Query rows at or below which the split phases run (WA_XATTN_SMALL_ROWS
+// overrides it: 0 = always fused; tests force each path).
+int xattn_small_rows() {
+  int v = 4;
+  if (const char* e = getenv("WA_XATTN_SMALL_ROWS")) v = atoi(e);
+  return std::max(0, std::min(kSmallRowsMax, v));
+}
+
 // 8 waves (two per SIMD, 256 registers each: the Z accumulators of an
 // eighth of the columns + one sub-chunk in flight); 4 when D / 8 is not a
 // multiple of 32 (D = 384).  A second sub-chunk in flight (PF = 2) does not
@@ -717,7 +1008,12 @@ XattnPlan xattn_plan(int R, int T) {
 
 size_t xattn_part_floats(int R, int H, int D, int T) {
   const XattnPlan p = xattn_plan(R, T);
-  return (size_t)R * p.splits * H * ((size_t)D + 2) + (size_t)R * H * D;
+  size_t n = (size_t)R * p.splits * H * ((size_t)D + 2) + (size_t)R * H * D;
+  if (R <= kSmallRowsMax) {  // split-phase scratch: scores, P planes, alpha, flags (+ 16-B alignment)
+    const size_t ng = (size_t)p.splits * p.ch;
+    n = (n + 3) / 4 * 4 + (size_t)R * ng * (32 * 16 + 32 * 16 + 32 + 1) + 4;
+  }
+  return n;
 }
 
 hipError_t launch_untile(const _Float16* tiled, int R, int K, int ns, float* out, hipStream_t st) {
@@ -757,14 +1053,21 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
     if (ns == 2) WA_XQ(2, kWtF16); else WA_XQ(1, kWtF16);
   }
 #undef WA_XQ
-  // stream the encoder output
+  // stream the encoder output: fused, or in split phases for few rows
   const dim3 gm(p.splits, R);
-#define WA_XMAIN(DD, HH)                                                          \
-  if (D == DD && HT == HH) {                                                      \
-    if (ns == 2)                                                                  \
-      launch_main<DD, HH, 2>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, R, st); \
-    else                                                                          \
-      launch_main<DD, HH, 1>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, R, st); \
+  const bool small = R <= xattn_small_rows() && p.ch <= kSmallMaxCH;
+  float* scratch = part + ((size_t)R * p.splits * H * ((size_t)D + 2) + (size_t)R * H * D + 3) / 4 * 4;
+#define WA_XMAIN(DD, HH)                                                                   \
+  if (D == DD && HT == HH) {                                                               \
+    if (small) {                                                                           \
+      if (ns == 2)                                                                         \
+        launch_small<DD, HH, 2>(R, Tq, T, H, p, qt, enc, z, ml, scratch, st);              \
+      else                                                                                 \
+        launch_small<DD, HH, 1>(R, Tq, T, H, p, qt, enc, z, ml, scratch, st);              \
+    } else if (ns == 2)                                                                    \
+      launch_main<DD, HH, 2>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, R, st);          \
+    else                                                                                   \
+      launch_main<DD, HH, 1>(gm, qt, enc, Tq, T, H, p.splits, p.ch, z, ml, R, st);          \
   } else
   WA_XMAIN(1280, 2)
   WA_XMAIN(1024, 1)
