@@ -475,8 +475,11 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
 // b + 16, b + 32) on VALU, 16 partials.  The partials are added through LDS
 // in a fixed order and out[r][h*64 + d] + bv goes into the A-tiled operand of
 // the output projection.  Fewer rows per workgroup spread the split-partial
-// stream (S * 5 KB per row and head) over more CUs.
-template <int NS, int WK, int RPW, int SM>
+// stream (S * 5 KB per row and head) over more CUs.  MTG > 1 (few rows, Q4
+// weights): the head's 64 outputs go to MTG workgroups (grid z), each staging
+// only its 64 / MTG weight rows and merging the rows' splits itself; every
+// output keeps its wave split and sum order, so its bits do not change.
+template <int NS, int WK, int RPW, int SM, int MTG>
 __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict__ zpart,
                                                         const float* __restrict__ mlpart, int R, int H, int D, int S,
                                                         const uint8_t* __restrict__ wv,
@@ -492,17 +495,19 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
   _Float16* zl = zh + RPW * ZLD;
   __shared__ __attribute__((aligned(16))) _Float16 zzero[8];
   __shared__ float red[16][64][RPW + 1];
-  const int h = blockIdx.x, rbase = blockIdx.y * RPW, rstep = 1;
+  static_assert(MTG == 1 || WK == kWtQ4, "output groups need the Q4 MFMA projection");
+  constexpr int NMT = 4 / MTG;  // 16-output m-tiles per workgroup
+  const int h = blockIdx.x, rbase = blockIdx.y * RPW, rstep = 1, mt0 = blockIdx.z * NMT;
   const int tid = threadIdx.x;
   const int nkb = D / 32;
   // the value bias of this thread's final outputs, loaded up front
-  const float bias1 = tid < 64 * RPW ? bv[h * 64 + (tid & 63)] : 0.0f;
+  const float bias1 = tid < 16 * NMT * RPW ? bv[h * 64 + 16 * mt0 + (tid & (16 * NMT - 1))] : 0.0f;
   const size_t rowbytes = (size_t)nkb * 18;
   if (WK == kWtQ4) {  // the head's 64 rows are contiguous: 64 * nkb * 18 bytes
-    const uint8_t* src = wv + (size_t)h * 64 * rowbytes;
+    const uint8_t* src = wv + ((size_t)h * 64 + 16 * mt0) * rowbytes;
     // LDS-DMA (global_load_lds_dwordx4): 1 KiB pieces straight into the
     // stage, every piece of a wave in flight at once (64 * 720 B = 45 KiB)
-    const int nbytes = (int)(64 * rowbytes);  // a multiple of 16 (64 * 18 * D / 32)
+    const int nbytes = (int)(16 * NMT * rowbytes);  // a multiple of 16 (16 * 18 * D / 32)
     const int w = tid >> 6, lane = tid & 63;
     for (int pc = w; pc * 1024 < nbytes; pc += 8)
       if (pc * 1024 + lane * 16 < nbytes) wq4::glds16(src + (size_t)pc * 1024 + lane * 16, &sw[pc * 1024]);
@@ -586,14 +591,14 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
     const int sh = (lq >> 1) * 4;
     floatx4 acc[4];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) acc[mt] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int mt = 0; mt < NMT; ++mt) acc[mt] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
     for (int kb = w; kb < nkb; kb += 8) {
       const _Float16* zhp = n < RPW ? &zh[n * ZLD + kb * 32 + 8 * lq] : zzero;
       const _Float16* zlp = n < RPW ? &zl[n * ZLD + kb * 32 + 8 * lq] : zzero;
       const half8 bh = *reinterpret_cast<const half8*>(zhp);
       const half8 bl = *reinterpret_cast<const half8*>(zlp);
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
+      for (int mt = 0; mt < NMT; ++mt) {  // local m-tile: outputs 16 (mt0 + mt) ..
         const uint16_t* blk = reinterpret_cast<const uint16_t*>(&sw[(size_t)(mt * 16 + n) * rowbytes + (size_t)kb * 18]);
         const _Float16 d = __builtin_bit_cast(_Float16, blk[0]) * (_Float16)kWvScale;  // exact: d < 16
         const half2v off = {(_Float16)1032.0f, (_Float16)1032.0f};
@@ -616,10 +621,10 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
         acc[mt] = mfma16x32(al, bh, acc[mt]);
       }
     }
-    // acc[mt][i]: output d = 16 mt + 4 lq + i, row n
+    // acc[mt][i]: output d = 16 (mt0 + mt) + 4 lq + i, row n (red indexed locally)
     if (n < RPW) {
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < NMT; ++mt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) red[w][16 * mt + 4 * lq + i][n] = acc[mt][i];
     }
@@ -653,13 +658,13 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
     }
   }
   __syncthreads();
-  if (tid < 64 * RPW) {  // thread (row j, output d): the block-group sum in group order, then 4-wide stores
-    const int j = tid >> 6, d = tid & 63, r = rbase + rstep * j;
+  if (tid < 16 * NMT * RPW) {  // thread (row j, output d): the block-group sum in group order, then 4-wide stores
+    const int j = tid / (16 * NMT), d = tid & (16 * NMT - 1), r = rbase + rstep * j;
     float sacc = bias1;
 #pragma unroll
     for (int g = 0; g < NPART; ++g) sacc += red[g][d][j] * (WK == kWtQ4 ? kOutInv : 1.0f);  // exact rescale
     const float v1 = __shfl_down(sacc, 1, 64), v2 = __shfl_down(sacc, 2, 64), v3 = __shfl_down(sacc, 3, 64);
-    if (r < R && (d & 3) == 0) atile_store4<NS>(tiled, r, h * 64 + d, kbp_of(D), sacc, v1, v2, v3);
+    if (r < R && (d & 3) == 0) atile_store4<NS>(tiled, r, h * 64 + 16 * mt0 + d, kbp_of(D), sacc, v1, v2, v3);
   }
 }
 
@@ -986,9 +991,16 @@ void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T,
 constexpr int kOutRows = 4;  // rows of Zn per xattn_out workgroup (measured: 4 beat 1, 2 and 8)
 template <int NS, int WK>
 void launch_out(dim3 go, const float* z, const float* ml, int R, int H, int D, int S, const uint8_t* wv,
-                const float* bv, _Float16* tiled, hipStream_t st) {
-  hipLaunchKernelGGL((xattn_out_kernel<NS, WK, kOutRows, kXattnSplits>), go, dim3(512), 0, st, z, ml, R, H, D, S, wv,
-                     bv, tiled);
+                const float* bv, _Float16* tiled, hipStream_t st, bool split_outputs = false) {
+  if constexpr (WK == kWtQ4) {
+    if (split_outputs) {  // few rows: 4 workgroups per head
+      hipLaunchKernelGGL((xattn_out_kernel<NS, WK, kOutRows, kXattnSplits, 4>), dim3(go.x, go.y, 4), dim3(512), 0, st,
+                         z, ml, R, H, D, S, wv, bv, tiled);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((xattn_out_kernel<NS, WK, kOutRows, kXattnSplits, 1>), go, dim3(512), 0, st, z, ml, R, H, D, S,
+                     wv, bv, tiled);
 }
 
 }  // namespace
@@ -1080,14 +1092,14 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   const dim3 go(H, (R + kOutRows - 1) / kOutRows);
   if (wtype == kWtQ4) {
     if (ns == 2)
-      launch_out<2, kWtQ4>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
+      launch_out<2, kWtQ4>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st, small);
     else
-      launch_out<1, kWtQ4>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
+      launch_out<1, kWtQ4>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st, small);
   } else {
     if (ns == 2)
-      launch_out<2, kWtF16>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
+      launch_out<2, kWtF16>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st, small);
     else
-      launch_out<1, kWtF16>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st);
+      launch_out<1, kWtF16>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st, small);
   }
   return hipGetLastError();
 }
