@@ -698,14 +698,14 @@ __global__ __launch_bounds__(256) void untile_kernel(const _Float16* __restrict_
 // ------------------------------------------- few query rows: split phases --
 // With R query rows the fused xattn_main_kernel runs S * R workgroups (8 at
 // one clip), each walking its CH sub-chunks in series (2.7 us each at 16
-// clips).  For R <= xattn_small_rows() the same arithmetic runs as three
+// clips).  For R <= xattn_small_rows() the same arithmetic runs as two
 // launches that spread over sub-chunks and columns instead:
 //   scores   one workgroup per (row, sub-chunk): the fused kernel's score
 //            MFMA sequence per wave column slice, its wave-order partial sum;
-//   softmax  one workgroup per (row, split): the fused kernel's online softmax
-//            step by step (same lanes, DPP reductions, rescale flag);
-//   z        one wave per (row, split, 32-column tile): the fused kernel's
-//            rescale + three MFMAs per sub-chunk on that tile.
+//   z        one workgroup per (row, split, 128 columns): the fused kernel's
+//            online softmax of the split (recomputed per workgroup while its
+//            encoder loads are in flight), then per wave one 32-column tile's
+//            rescale + three MFMAs per sub-chunk.
 // Every partial (Z, max, sum) therefore has the fused path's bits, so a
 // clip's tokens do not depend on the batch (test_xattn_small_rows_bit_identical).
 constexpr int kSmallMaxCH = 12;   // sub-chunks per split the softmax/z kernels preload (T <= 1536 at 8 splits)
@@ -779,83 +779,18 @@ __global__ __launch_bounds__(64 * NW) void xattn_scores_kernel(const _Float16* _
   }
 }
 
-// pbuf [row][sub-chunk][NS][32 heads][16 frames] f16 (P * 2^15 split), abuf
-// [row][sub-chunk][32] alpha.  Every head's 16 lanes run on their own: no
-// barrier (the rescale flag is derived from the alphas by the z kernel).
-template <int HT, int NS, int NW>
-__global__ __launch_bounds__(64 * NW) void xattn_softmax_kernel(const float* __restrict__ sbuf, int T, int H, int S,
-                                                                int CH, int NG, _Float16* __restrict__ pbuf,
-                                                                float* __restrict__ abuf, float* __restrict__ mlpart) {
-  constexpr int kThreads = 64 * NW, HP = HT * 16;
-  constexpr int SMX = 512 / kThreads;  // entries (head 0..31, frame) per thread
-  const int s = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
-  const int ts = s * CH * kTc, te = min(T, ts + CH * kTc);
-  const int nch = te > ts ? (te - ts + kTc - 1) / kTc : 0;
-  float sv_all[kSmallMaxCH][SMX];
-#pragma unroll
-  for (int c = 0; c < kSmallMaxCH; ++c)
-#pragma unroll
-    for (int e = 0; e < SMX; ++e) {
-      const int idx = tid + e * kThreads, h = idx >> 4, t = idx & 15;
-      const int cc = c < nch ? c : 0, hc = h < HP ? h : 0;  // every load issued up front (no branch)
-      sv_all[c][e] = sbuf[(((size_t)r * NG + s * CH + cc) * HP + hc) * 16 + t];
-    }
-  float M[SMX], L[SMX];
-#pragma unroll
-  for (int e = 0; e < SMX; ++e) {
-    M[e] = -INFINITY;
-    L[e] = 0.0f;
-  }
-#pragma unroll
-  for (int chi = 0; chi < kSmallMaxCH; ++chi) {
-    if (chi >= nch) break;
-    const int t0 = ts + chi * kTc;
-    const size_t gi = (size_t)r * NG + s * CH + chi;
-#pragma unroll
-    for (int e = 0; e < SMX; ++e) {
-      const int idx = tid + e * kThreads, h = idx >> 4, t = idx & 15;
-      _Float16 phi = (_Float16)0.0f, plo = (_Float16)0.0f;
-      float alpha = 1.0f;
-      if (h < HP) {  // the fused kernel's softmax entry, verbatim
-        float sv = sv_all[chi][e];
-        const bool valid = h < H && t0 + t < te;
-        sv = valid ? sv : -INFINITY;
-        const float cm = wq4::max16(sv);
-        const float mn = fmaxf(M[e], cm);
-        float p = 0.0f;
-        if (mn != -INFINITY) {
-          alpha = __builtin_amdgcn_exp2f((M[e] - mn) * kSInv);
-          p = valid ? __builtin_amdgcn_exp2f((sv - mn) * kSInv) : 0.0f;
-        }
-        const float ps = wq4::sum16(p);
-        L[e] = L[e] * alpha + ps;
-        M[e] = mn;
-        split_f16(p * kPScale, phi, plo);
-      }
-      pbuf[((gi * NS + 0) * 32 + h) * 16 + t] = phi;
-      if (NS == 2) pbuf[((gi * NS + 1) * 32 + h) * 16 + t] = plo;
-      if (t == 0) abuf[gi * 32 + h] = alpha;
-    }
-  }
-  const size_t base = (size_t)r * S + s;
-#pragma unroll
-  for (int e = 0; e < SMX; ++e) {
-    const int idx = tid + e * kThreads, h = idx >> 4;
-    if ((idx & 15) == 0 && h < H && h < HP) {
-      mlpart[(base * H + h) * 2] = M[e] * kSInv;
-      mlpart[(base * H + h) * 2 + 1] = L[e];
-    }
-  }
-}
-
-// grid (S, D / 128, R), 4 waves: wave w owns columns cb .. cb + 31 of split s
-template <int D, int NS>
+// grid (S, D / 128, R), 4 waves: wave w owns columns cb .. cb + 31 of split
+// s.  The split's online softmax (the fused kernel's, step by step: same
+// lanes, DPP reductions, rescale flag) is recomputed by every workgroup of
+// the split from the scores while its encoder loads are in flight; the
+// workgroup of column group 0 writes the split's (max, sum).
+template <int D, int HT, int NS>
 __global__ __launch_bounds__(256) void xattn_z_kernel(const _Float16* __restrict__ enc,
-                                                      const _Float16* __restrict__ pbuf,
-                                                      const float* __restrict__ abuf,
-                                                      int Tq, int T, int H, int S, int CH, int NG,
-                                                      float* __restrict__ zpart) {
-  constexpr int ROW = NS * D, ZR = 32;  // staged plane: 16 frames x 32 columns, rows of 64 B
+                                                      const float* __restrict__ sbuf, int Tq, int T, int H, int S,
+                                                      int CH, int NG, float* __restrict__ zpart,
+                                                      float* __restrict__ mlpart) {
+  constexpr int ROW = NS * D, ZR = 32, HP = HT * 16;  // staged plane: 16 frames x 32 columns, rows of 64 B
+  constexpr int SMX = 512 / 256;                      // softmax entries (head 0..31, frame) per thread
   __shared__ __attribute__((aligned(16))) _Float16 sp[kSmallMaxCH][NS][32][kTc];
   __shared__ float sal[kSmallMaxCH][32];
   __shared__ int sfl[kSmallMaxCH];
@@ -877,39 +812,66 @@ __global__ __launch_bounds__(256) void xattn_z_kernel(const _Float16* __restrict
   for (int c = 0; c < kSmallMaxCH; ++c)
 #pragma unroll
     for (int p = 0; p < NS; ++p)  // unconditional: past the split's frames the buffer gives zeros
-        ev[c][p] = __builtin_amdgcn_raw_buffer_load_b128(
-            rs, (uint32_t)((((c * kTc + (l >> 2)) * ROW) + p * D + cb + 8 * (l & 3)) * 2), 0, 0);
-  // P and alpha of the split (shared by the 4 waves): every load issued
-  // before any is stored; the rescale flag of a sub-chunk = some alpha != 1
-  // (the fused kernel's srescale)
-  constexpr int NPV = kSmallMaxCH * NS * 32 * kTc / 8 / 256;  // half8 per thread
-  constexpr int NAV = (kSmallMaxCH * 32 + 255) / 256;
-  half8 pv[NPV];
-  float av[NAV];
-  const int npv = nch * NS * 32 * kTc / 8, nav = nch * 32;
+      ev[c][p] = __builtin_amdgcn_raw_buffer_load_b128(
+          rs, (uint32_t)((((c * kTc + (l >> 2)) * ROW) + p * D + cb + 8 * (l & 3)) * 2), 0, 0);
+  // the split's scores (every load issued up front)
+  float sv_all[kSmallMaxCH][SMX];
 #pragma unroll
-  for (int u = 0; u < NPV; ++u) {
-    const int i = tid + 256 * u;
-    pv[u] = reinterpret_cast<const half8*>(pbuf + g0 * NS * 32 * kTc)[i < npv ? i : 0];
-  }
+  for (int c = 0; c < kSmallMaxCH; ++c)
 #pragma unroll
-  for (int u = 0; u < NAV; ++u) {
-    const int i = tid + 256 * u;
-    av[u] = abuf[g0 * 32 + (i < nav ? i : 0)];
-  }
+    for (int e = 0; e < SMX; ++e) {
+      const int idx = tid + e * 256, h = idx >> 4, t = idx & 15;
+      const int cc = c < nch ? c : 0, hc = h < HP ? h : 0;
+      sv_all[c][e] = sbuf[((g0 + cc) * HP + hc) * 16 + t];
+    }
   if (tid < kSmallMaxCH) sfl[tid] = 0;
   __syncthreads();
+  float M[SMX], L[SMX];
 #pragma unroll
-  for (int u = 0; u < NPV; ++u) {
-    const int i = tid + 256 * u;
-    if (i < npv) reinterpret_cast<half8*>(&sp[0][0][0][0])[i] = pv[u];
+  for (int e = 0; e < SMX; ++e) {
+    M[e] = -INFINITY;
+    L[e] = 0.0f;
   }
 #pragma unroll
-  for (int u = 0; u < NAV; ++u) {
-    const int i = tid + 256 * u;
-    if (i < nav) {
-      (&sal[0][0])[i] = av[u];
-      if (av[u] != 1.0f) sfl[i >> 5] = 1;  // benign race: every writer stores 1
+  for (int chi = 0; chi < kSmallMaxCH; ++chi) {
+    if (chi >= nch) continue;
+    const int t0 = ts + chi * kTc;
+#pragma unroll
+    for (int e = 0; e < SMX; ++e) {
+      const int idx = tid + e * 256, h = idx >> 4, t = idx & 15;
+      _Float16 phi = (_Float16)0.0f, plo = (_Float16)0.0f;
+      float alpha = 1.0f;
+      if (h < HP) {  // the fused kernel's softmax entry, verbatim
+        float sv = sv_all[chi][e];
+        const bool valid = h < H && t0 + t < te;
+        sv = valid ? sv : -INFINITY;
+        const float cm = wq4::max16(sv);
+        const float mn = fmaxf(M[e], cm);
+        float p = 0.0f;
+        if (mn != -INFINITY) {
+          alpha = __builtin_amdgcn_exp2f((M[e] - mn) * kSInv);
+          p = valid ? __builtin_amdgcn_exp2f((sv - mn) * kSInv) : 0.0f;
+        }
+        const float ps = wq4::sum16(p);
+        L[e] = L[e] * alpha + ps;
+        M[e] = mn;
+        split_f16(p * kPScale, phi, plo);
+      }
+      sp[chi][0][h][t] = phi;
+      if (NS == 2) sp[chi][1][h][t] = plo;
+      if (t == 0) sal[chi][h] = alpha;
+      if (alpha != 1.0f) sfl[chi] = 1;  // benign race: every writer stores 1
+    }
+  }
+  if (blockIdx.y == 0) {
+    const size_t base = (size_t)r * S + s;
+#pragma unroll
+    for (int e = 0; e < SMX; ++e) {
+      const int idx = tid + e * 256, h = idx >> 4;
+      if ((idx & 15) == 0 && h < H && h < HP) {
+        mlpart[(base * H + h) * 2] = M[e] * kSInv;
+        mlpart[(base * H + h) * 2 + 1] = L[e];
+      }
     }
   }
   __syncthreads();
@@ -957,14 +919,10 @@ void launch_small(int R, int Tq, int T, int H, const XattnPlan& p, const _Float1
                   float* z, float* ml, float* scratch, hipStream_t st) {
   constexpr int NW = (D / 8) % 32 == 0 ? 8 : 4;
   const int NG = p.splits * p.ch;
-  float* sb = scratch;                                                       // R * NG * 32 * 16 floats
-  _Float16* pb = reinterpret_cast<_Float16*>(sb + (size_t)R * NG * 32 * 16);  // R * NG * 2 * 32 * 16 halves
-  float* ab = reinterpret_cast<float*>(pb + (size_t)R * NG * 2 * 32 * 16);    // R * NG * 32
+  float* sb = scratch;  // R * NG * 32 * 16 floats
   hipLaunchKernelGGL((xattn_scores_kernel<D, HT, NS, NW>), dim3(NG, R), dim3(64 * NW), 0, st, qt, enc, Tq, T, NG, sb);
-  hipLaunchKernelGGL((xattn_softmax_kernel<HT, NS, NW>), dim3(p.splits, R), dim3(64 * NW), 0, st, sb, T, H,
-                     p.splits, p.ch, NG, pb, ab, ml);
-  hipLaunchKernelGGL((xattn_z_kernel<D, NS>), dim3(p.splits, D / 128, R), dim3(256), 0, st, enc, pb, ab, Tq, T,
-                     H, p.splits, p.ch, NG, z);
+  hipLaunchKernelGGL((xattn_z_kernel<D, HT, NS>), dim3(p.splits, D / 128, R), dim3(256), 0, st, enc, sb, Tq, T, H,
+                     p.splits, p.ch, NG, z, ml);
 }
 
 // Query rows at or below which the split phases run (WA_XATTN_SMALL_ROWS
@@ -1021,9 +979,9 @@ XattnPlan xattn_plan(int R, int T) {
 size_t xattn_part_floats(int R, int H, int D, int T) {
   const XattnPlan p = xattn_plan(R, T);
   size_t n = (size_t)R * p.splits * H * ((size_t)D + 2) + (size_t)R * H * D;
-  if (R <= kSmallRowsMax) {  // split-phase scratch: scores, P planes, alpha, flags (+ 16-B alignment)
+  if (R <= kSmallRowsMax) {  // split-phase scratch: the scores (+ 16-B alignment)
     const size_t ng = (size_t)p.splits * p.ch;
-    n = (n + 3) / 4 * 4 + (size_t)R * ng * (32 * 16 + 32 * 16 + 32 + 1) + 4;
+    n = (n + 3) / 4 * 4 + (size_t)R * ng * 32 * 16 + 4;
   }
   return n;
 }

@@ -95,26 +95,20 @@ int main(int argc, char** argv) {
     const float t_all = time_it([&] {
       wa::launch_xattn(q, wk, wv, bv, wa::kWtQ4, enc, R, 1, T, H, D, qt, part, tiled, NS, 0);
     });
-    float t_sc = 0.0f, t_sm = 0.0f, t_z = 0.0f;
+    float t_sc = 0.0f, t_z = 0.0f;
     if (R <= wa::kSmallRowsMax) {  // the split phases one by one
       const int NG = p.splits * p.ch;
       float* sb = part + ((size_t)R * p.splits * H * ((size_t)D + 2) + (size_t)R * H * D + 3) / 4 * 4;
-      _Float16* pb = reinterpret_cast<_Float16*>(sb + (size_t)R * NG * 32 * 16);
-      float* ab = reinterpret_cast<float*>(pb + (size_t)R * NG * 2 * 32 * 16);
       t_sc = time_it([&] {
         hipLaunchKernelGGL((wa::xattn_scores_kernel<1280, 2, 2, 8>), dim3(NG, R), dim3(512), 0, 0, qt, enc, 1, T, NG, sb);
       });
-      t_sm = time_it([&] {
-        hipLaunchKernelGGL((wa::xattn_softmax_kernel<2, 2, 8>), dim3(p.splits, R), dim3(512), 0, 0, sb, T, H, p.splits,
-                           p.ch, NG, pb, ab, ml);
-      });
       t_z = time_it([&] {
-        hipLaunchKernelGGL((wa::xattn_z_kernel<1280, 2>), dim3(p.splits, D / 128, R), dim3(256), 0, 0, enc, pb, ab,
-                           1, T, H, p.splits, p.ch, NG, z);
+        hipLaunchKernelGGL((wa::xattn_z_kernel<1280, 2, 2>), dim3(p.splits, D / 128, R), dim3(256), 0, 0, enc, sb, 1, T,
+                           H, p.splits, p.ch, NG, z, ml);
       });
     }
     CK(hipGetLastError());
-    printf("{\"rows\": %d, \"scores_us\": %.2f, \"softmax_us\": %.2f, \"z_us\": %.2f}\n", R, t_sc, t_sm, t_z);
+    printf("{\"rows\": %d, \"scores_us\": %.2f, \"z_us\": %.2f}\n", R, t_sc, t_z);
     const double bytes = (double)R * T * D * 2 * NS;
     printf("{\"small\": %d, \"diag\": %d, \"rows\": %d, \"splits\": %d, \"main_us\": %.2f, \"q_us\": %.2f, \"out_us\": %.2f, "
            "\"all_us\": %.2f, \"main_tbs\": %.3f}\n",
