@@ -92,6 +92,11 @@ int main(int argc, char** argv) {
       wa::launch_out<2, wa::kWtQ4>(dim3(H, (R + wa::kOutRows - 1) / wa::kOutRows), z, ml, R, H, D, p.splits, wv, bv,
                                    tiled, 0);
     });
+    const float t_out4 = time_it([&] {
+      wa::launch_out<2, wa::kWtQ4>(dim3(H, (R + wa::kOutRows - 1) / wa::kOutRows), z, ml, R, H, D, p.splits, wv, bv,
+                                   tiled, 0, true);
+    });
+    printf("{\"rows\": %d, \"out_split4_us\": %.2f}\n", R, t_out4);
     const float t_all = time_it([&] {
       wa::launch_xattn(q, wk, wv, bv, wa::kWtQ4, enc, R, 1, T, H, D, qt, part, tiled, NS, 0);
     });
