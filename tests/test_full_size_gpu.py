@@ -134,3 +134,50 @@ def test_full_size_encoder_and_prompt_logits(name):
     err = float(np.max(np.abs(lg[keep] - p64[keep])))
     assert err <= tol, f"{name}: prompt logits |gpu - f64| {err:.3e} > {tol:.3e}"
     m.close()
+
+
+# --precision f16 (one MFMA per multiply-add: every multiplicand rounded to an
+# f16, 2^-11, where f32 rounds to 2^-24; accumulation stays f32): the logit
+# bound scales the f32 oracle's error by 2048 (a quarter of the operand
+# rounding ratio 8192) with a floor of 5e-4 (about one f16 ulp) of the
+# logits' magnitude.  Tokens must still equal the f32 oracle's.
+RATIO_F16 = 2048.0
+FLOOR_F16 = 5e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_full_size_tokens_f16_precision(name):
+    """BASELINE's bf16-class arithmetic (f16 operands, f32 MFMA accumulation,
+    the mode `bench.py --precision f16` times): emitted tokens equal the f32
+    oracle's on every fixture, logits within the f16 bound stated above."""
+    import torch
+
+    import whisper_amd
+    import wq4
+    from whisper_oracle import synthetic_mel
+
+    f, meta = _fixture(name)
+    clips, steps, lang = meta["clips"], meta["steps"], meta["lang"]
+    B = len(clips)
+    m = whisper_amd.WhisperModel(meta["variant"], meta["seed"], max_batch=B, weights=meta["weights"],
+                                 precision=wq4.PREC_F16)
+    mel = torch.from_numpy(np.stack([synthetic_mel(c, m.config["n_mels"]) for c in clips])).cuda()
+    toks, lg = m.transcribe_trace(mel, f["top_ids"], lang, steps, eot_stop=False)
+    ref = f["tokens_f32"]
+    flips = [(b, s, int(toks[b][s]), int(ref[b, s]), float(f["margin_f32"][b, s]))
+             for b in range(B) for s in range(steps) if toks[b][s] != ref[b, s]]
+    assert not flips, f"{name} (f16): {len(flips)} token flips; first {sorted(flips, key=lambda x: x[1])[:4]}"
+    got = lg[:, 1:, :].astype(np.float64)
+    r32, r64 = f["top_f32"][:, 1:, :], f["top_f64"][:, 1:, :]
+    worst = 0.0
+    for b in range(B):
+        for s in range(steps):
+            k = np.isfinite(r64[b, s])
+            e_ref = float(np.max(np.abs(r32[b, s, k].astype(np.float64) - r64[b, s, k])))
+            tol = RATIO_F16 * e_ref + FLOOR_F16 * float(np.max(np.abs(r64[b, s, k])))
+            err = float(np.max(np.abs(got[b, s, k] - r64[b, s, k])))
+            worst = max(worst, err / tol)
+            assert err <= tol, f"{name} (f16): clip {b} step {s + 1}: |gpu - f64| {err:.3e} > {tol:.3e}"
+    print(f"{name} (f16): tokens equal ({B} x {steps}), worst logit error {worst:.3f} of the f16 bound")
+    m.close()
