@@ -946,19 +946,42 @@ void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T,
     hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 4, 1>), g, dim3(256), 0, st, qt, enc, Tq, T, H, S, CH, z, ml, R);
 }
 
-constexpr int kOutRows = 4;  // rows of Zn per xattn_out workgroup (measured: 4 beat 1, 2 and 8)
-template <int NS, int WK>
-void launch_out(dim3 go, const float* z, const float* ml, int R, int H, int D, int S, const uint8_t* wv,
-                const float* bv, _Float16* tiled, hipStream_t st, bool split_outputs = false) {
+// Rows of Zn per xattn_out workgroup: 4.  Isolated, 2 rows per workgroup is
+// faster at 16 rows (9.6 vs 11.0 us) and slower at 32 (14.3 vs 11.1); in the
+// model (two concurrent 16-row decode groups) 2 rows made the decode slower
+// (893-898 vs 874-878 ms, scripts/gpu_ab_outrows.sh): the doubled grid
+// crowds the other group.  1 and 8 are slower everywhere.  A row's bits do
+// not depend on its workgroup's rows (each is its own MFMA column).
+#ifndef WA_XATTN_OUT_ROWS  // compile-time override: tuning builds (scripts/xattn_micro.sh)
+#define WA_XATTN_OUT_ROWS 4
+#endif
+int out_rows(int R) {
+  (void)R;
+  return WA_XATTN_OUT_ROWS;
+}
+template <int NS, int WK, int RPW>
+void launch_out_rpw(int R, int H, const float* z, const float* ml, int D, int S, const uint8_t* wv, const float* bv,
+                    _Float16* tiled, hipStream_t st, bool split_outputs) {
+  const dim3 go(H, (R + RPW - 1) / RPW);
   if constexpr (WK == kWtQ4) {
     if (split_outputs) {  // few rows: 4 workgroups per head
-      hipLaunchKernelGGL((xattn_out_kernel<NS, WK, kOutRows, kXattnSplits, 4>), dim3(go.x, go.y, 4), dim3(512), 0, st,
-                         z, ml, R, H, D, S, wv, bv, tiled);
+      hipLaunchKernelGGL((xattn_out_kernel<NS, WK, RPW, kXattnSplits, 4>), dim3(go.x, go.y, 4), dim3(512), 0, st, z,
+                         ml, R, H, D, S, wv, bv, tiled);
       return;
     }
   }
-  hipLaunchKernelGGL((xattn_out_kernel<NS, WK, kOutRows, kXattnSplits, 1>), go, dim3(512), 0, st, z, ml, R, H, D, S,
-                     wv, bv, tiled);
+  hipLaunchKernelGGL((xattn_out_kernel<NS, WK, RPW, kXattnSplits, 1>), go, dim3(512), 0, st, z, ml, R, H, D, S, wv,
+                     bv, tiled);
+}
+template <int NS, int WK>
+void launch_out(int R, int H, const float* z, const float* ml, int D, int S, const uint8_t* wv, const float* bv,
+                _Float16* tiled, hipStream_t st, bool split_outputs = false) {
+  switch (out_rows(R)) {
+    case 1: launch_out_rpw<NS, WK, 1>(R, H, z, ml, D, S, wv, bv, tiled, st, split_outputs); break;
+    case 2: launch_out_rpw<NS, WK, 2>(R, H, z, ml, D, S, wv, bv, tiled, st, split_outputs); break;
+    case 8: launch_out_rpw<NS, WK, 8>(R, H, z, ml, D, S, wv, bv, tiled, st, split_outputs); break;
+    default: launch_out_rpw<NS, WK, 4>(R, H, z, ml, D, S, wv, bv, tiled, st, split_outputs); break;
+  }
 }
 
 }  // namespace
@@ -1047,17 +1070,16 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   return hipErrorInvalidValue;
 #undef WA_XMAIN
   // merge the splits and project with Wv into the output projection's operand
-  const dim3 go(H, (R + kOutRows - 1) / kOutRows);
   if (wtype == kWtQ4) {
     if (ns == 2)
-      launch_out<2, kWtQ4>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st, small);
+      launch_out<2, kWtQ4>(R, H, z, ml, D, p.splits, wv, bv, tiled, st, small);
     else
-      launch_out<1, kWtQ4>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st, small);
+      launch_out<1, kWtQ4>(R, H, z, ml, D, p.splits, wv, bv, tiled, st, small);
   } else {
     if (ns == 2)
-      launch_out<2, kWtF16>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st, small);
+      launch_out<2, kWtF16>(R, H, z, ml, D, p.splits, wv, bv, tiled, st, small);
     else
-      launch_out<1, kWtF16>(go, z, ml, R, H, D, p.splits, wv, bv, tiled, st, small);
+      launch_out<1, kWtF16>(R, H, z, ml, D, p.splits, wv, bv, tiled, st, small);
   }
   return hipGetLastError();
 }

@@ -89,12 +89,10 @@ int main(int argc, char** argv) {
                          q, R, D, wk, HP, qt);
     });
     const float t_out = time_it([&] {
-      wa::launch_out<2, wa::kWtQ4>(dim3(H, (R + wa::kOutRows - 1) / wa::kOutRows), z, ml, R, H, D, p.splits, wv, bv,
-                                   tiled, 0);
+      wa::launch_out<2, wa::kWtQ4>(R, H, z, ml, D, p.splits, wv, bv, tiled, 0);
     });
     const float t_out4 = time_it([&] {
-      wa::launch_out<2, wa::kWtQ4>(dim3(H, (R + wa::kOutRows - 1) / wa::kOutRows), z, ml, R, H, D, p.splits, wv, bv,
-                                   tiled, 0, true);
+      wa::launch_out<2, wa::kWtQ4>(R, H, z, ml, D, p.splits, wv, bv, tiled, 0, true);
     });
     printf("{\"rows\": %d, \"out_split4_us\": %.2f}\n", R, t_out4);
     const float t_all = time_it([&] {
