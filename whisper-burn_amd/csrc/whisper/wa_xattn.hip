@@ -49,11 +49,11 @@ constexpr float kXqScale = 0.125f * 1.4426950408889634f;  // 1 / sqrt(64) * log2
 // wq4_device.hpp split_act), all powers of two, undone in f32 (exact):
 //   xattn_q   q rows x 2^4 (split_act), Wk x 2^12 (|w| < 16), product x 2^-16
 //   main      qt x 2^5, encoder planes x 2^5 (|x| < 2047): scores x 2^10;
-//             p in (0, 1] x 2^15: Z x 2^20
+//             p in (0, 2] x 2^14 (the lazy reference maximum, softmax_entry): Z x 2^19
 //   out       Zn x 2^5, Wv scale d x 2^12 (d < 16): product x 2^-17
 constexpr float kWkScale = 4096.0f, kXqInv = 1.0f / (16.0f * 4096.0f);
 constexpr float kQtScale = 32.0f, kEncScale = 32.0f, kSInv = 1.0f / 1024.0f;
-constexpr float kPScale = 32768.0f, kZInv = 1.0f / (32768.0f * 32.0f);
+constexpr float kPScale = 16384.0f, kZInv = 1.0f / (16384.0f * 32.0f);
 constexpr float kZnScale = 32.0f, kWvScale = 4096.0f, kOutInv = 1.0f / (32.0f * 4096.0f);
 #ifndef WA_XATTN_SPLITS  // compile-time only: tuning builds of scripts/gpu_xattn_splits.sh
 #define WA_XATTN_SPLITS 8
@@ -187,6 +187,30 @@ __global__ __launch_bounds__(128) void xattn_q_mfma_kernel(const float* __restri
       if (NS == 2) qt[(((size_t)r * NS + 1) * HP + h) * D + c0 + c] = y;
     }
   }
+}
+
+// One (head, frame) entry of the online softmax over a 16-frame sub-chunk,
+// shared by the fused and the split-phase kernels (their bits must agree):
+// the head's 16 lanes form one DPP row.  Scores carry the 2^10 operand scale.
+// Lazy reference maximum: the running reference M only moves when the
+// sub-chunk's maximum exceeds it by more than 1 (base 2), so p <= 2 and most
+// sub-chunks need no rescale of Z (alpha == 1 exactly); any reference gives
+// the same softmax, and xattn_out's merge uses the references it is given.
+constexpr float kLazyMax = 1024.0f;  // 1.0 in base-2 units x 2^10
+__device__ __forceinline__ void softmax_entry(float sv, bool valid, float& M, float& L, float& alpha, float& p) {
+  sv = valid ? sv : -INFINITY;
+  const float cm = wq4::max16(sv);  // DPP butterfly over the head's 16 frames
+  float mn = fmaxf(M, cm);
+  if (M != -INFINITY && mn - M <= kLazyMax) mn = M;
+  alpha = 1.0f;
+  p = 0.0f;
+  if (mn != -INFINITY) {
+    alpha = __builtin_amdgcn_exp2f((M - mn) * kSInv);
+    p = valid ? __builtin_amdgcn_exp2f((sv - mn) * kSInv) : 0.0f;
+  }
+  const float ps = wq4::sum16(p);
+  L = L * alpha + ps;
+  M = mn;
 }
 
 // ------------------------------------------------------------ main stream --
@@ -363,19 +387,10 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
 #pragma unroll
         for (int ww = 0; ww < NW; ++ww) sv += red[ww][ht][hh][t];
         const bool valid = h < H && t0 + t < te;
-        sv = valid ? sv : -INFINITY;
-        const float cm = wq4::max16(sv);  // DPP butterfly over the head's 16 frames
-        const float mn = fmaxf(M[e], cm);  // scores (and M) carry the 2^10 operand scale
-        float alpha = 1.0f, p = 0.0f;
-        if (mn != -INFINITY) {
-          alpha = __builtin_amdgcn_exp2f((M[e] - mn) * kSInv);
-          p = valid ? __builtin_amdgcn_exp2f((sv - mn) * kSInv) : 0.0f;
-        }
-        const float ps = wq4::sum16(p);
-        L[e] = L[e] * alpha + ps;
-        M[e] = mn;
+        float alpha, p;
+        softmax_entry(sv, valid, M[e], L[e], alpha, p);
         _Float16 phi, plo;
-        split_f16(p * kPScale, phi, plo);  // p * 2^15: the lo half stays a normal f16 (undone at the store)
+        split_f16(p * kPScale, phi, plo);  // p * 2^14: the lo half stays a normal f16 (undone at the store)
         if (WA_XATTN_DIAG == 8) phi = plo = (_Float16)0.0f;
         sp[0][h][t] = phi;
         if (NS == 2) sp[1][h][t] = plo;
@@ -841,20 +856,9 @@ __global__ __launch_bounds__(256) void xattn_z_kernel(const _Float16* __restrict
       const int idx = tid + e * 256, h = idx >> 4, t = idx & 15;
       _Float16 phi = (_Float16)0.0f, plo = (_Float16)0.0f;
       float alpha = 1.0f;
-      if (h < HP) {  // the fused kernel's softmax entry, verbatim
-        float sv = sv_all[chi][e];
-        const bool valid = h < H && t0 + t < te;
-        sv = valid ? sv : -INFINITY;
-        const float cm = wq4::max16(sv);
-        const float mn = fmaxf(M[e], cm);
-        float p = 0.0f;
-        if (mn != -INFINITY) {
-          alpha = __builtin_amdgcn_exp2f((M[e] - mn) * kSInv);
-          p = valid ? __builtin_amdgcn_exp2f((sv - mn) * kSInv) : 0.0f;
-        }
-        const float ps = wq4::sum16(p);
-        L[e] = L[e] * alpha + ps;
-        M[e] = mn;
+      if (h < HP) {  // the fused kernel's softmax entry
+        float p;
+        softmax_entry(sv_all[chi][e], h < H && t0 + t < te, M[e], L[e], alpha, p);
         split_f16(p * kPScale, phi, plo);
       }
       sp[chi][0][h][t] = phi;
