@@ -2,7 +2,9 @@
 clips (encoder + two-group decode) while model B, on its own CU-masked
 stream (WA_ENC_CU_MASK=N at its creation), runs encoders back to back in a
 second thread.  Prints A's phase times alone and with B running, and B's
-encoder time alone and under A's decode.   python3 scripts/overlap_probe.py N"""
+encoder time alone and under A's decode.   python3 scripts/overlap_probe.py N
+(WA_ENC_CU_MASK lived in the r02 experiment build of wa_model.cpp only: the
+mask did not restrict the encoder, DESIGN.md §4 dead ends.)"""
 import os
 import sys
 import threading
