@@ -73,6 +73,11 @@ constexpr int kXattnSplits = WA_XATTN_SPLITS;
 #ifndef WA_XATTN_DIAG
 #define WA_XATTN_DIAG 0
 #endif
+// xattn_out attribution builds (tools/xattn_micro.hip only, wrong results):
+// 1 = no Wv stage, 2 = no split-partial loads, 3 = no projection MFMAs.
+#ifndef WA_XATTN_ODIAG
+#define WA_XATTN_ODIAG 0
+#endif
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -524,7 +529,7 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
     // stage, every piece of a wave in flight at once (64 * 720 B = 45 KiB)
     const int nbytes = (int)(16 * NMT * rowbytes);  // a multiple of 16 (16 * 18 * D / 32)
     const int w = tid >> 6, lane = tid & 63;
-    for (int pc = w; pc * 1024 < nbytes; pc += 8)
+    for (int pc = w; pc * 1024 < nbytes && WA_XATTN_ODIAG != 1; pc += 8)
       if (pc * 1024 + lane * 16 < nbytes) wq4::glds16(src + (size_t)pc * 1024 + lane * 16, &sw[pc * 1024]);
   }
   // merge of the S frame ranges (flash-attention merge, fixed split order):
@@ -549,8 +554,8 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
 #pragma unroll
       for (int s = 0; s < SM; ++s)
         if (s < S) {
-          ml[u][s] = mp[(size_t)s * H];
-          zv[u][s] = zp[(size_t)s * H * (D / 4)];
+          ml[u][s] = WA_XATTN_ODIAG == 2 ? floatx2{0.0f, 1.0f} : mp[(size_t)s * H];
+          zv[u][s] = WA_XATTN_ODIAG == 2 ? floatx4{0.0f, 0.0f, 0.0f, 0.0f} : zp[(size_t)s * H * (D / 4)];
         }
     }
 #pragma unroll
@@ -607,7 +612,7 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
     floatx4 acc[4];
 #pragma unroll
     for (int mt = 0; mt < NMT; ++mt) acc[mt] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-    for (int kb = w; kb < nkb; kb += 8) {
+    for (int kb = w; kb < (WA_XATTN_ODIAG == 3 ? 0 : nkb); kb += 8) {
       const _Float16* zhp = n < RPW ? &zh[n * ZLD + kb * 32 + 8 * lq] : zzero;
       const _Float16* zlp = n < RPW ? &zl[n * ZLD + kb * 32 + 8 * lq] : zzero;
       const half8 bh = *reinterpret_cast<const half8*>(zhp);
