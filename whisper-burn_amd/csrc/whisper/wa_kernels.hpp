@@ -43,8 +43,13 @@ struct XattnPlan {
 };
 XattnPlan xattn_plan(int R, int T);
 size_t xattn_part_floats(int R, int H, int D, int T);
-hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, const float* bv, int wtype,
-                        const _Float16* enc, int B, int Tq, int T, int H, int D, _Float16* qt, float* part,
+// Q4_0 Wv repacked once at model load into the cross-attention
+// projection's lane order (same bytes; wv_pack_words u32 words).
+size_t wv_pack_words(int H, int D);
+hipError_t launch_wv_pack(const uint8_t* wv, int H, int D, uint32_t* out, hipStream_t st);
+// wvp: the launch_wv_pack words of wv (Q4 weights; ignored for f16 weights)
+hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, const uint32_t* wvp, const float* bv,
+                        int wtype, const _Float16* enc, int B, int Tq, int T, int H, int D, _Float16* qt, float* part,
                         _Float16* tiled, int ns, hipStream_t st);
 // A-tiled operand [R][K] (hi + lo) -> f32 rows (diagnostics).
 hipError_t launch_untile(const _Float16* tiled, int R, int K, int ns, float* out, hipStream_t st);

@@ -155,6 +155,7 @@ struct DecLayer {
   // cross-attention key / value weights in raw GGUF form (Q4_0 blocks or
   // f16), read by the K/V-cache-free cross-attention (wa_xattn.hip)
   uint8_t *ck_raw = nullptr, *cv_raw = nullptr;
+  uint32_t* cv_p = nullptr;  // Q4_0: cv_raw in the projection's lane order (wa::launch_wv_pack)
   float *cache_k, *cache_v;
 };
 
@@ -517,6 +518,13 @@ wq4_status build_model(wa_model* m, Source& src) {
     // in Whisper, cancels in the softmax and is not needed)
     L.ck_raw = B.raw(p + ".cross_attn.key.weight", Dt, D);
     L.cv_raw = B.raw(p + ".cross_attn.value.weight", Dt, D);
+    if (L.cv_raw && m->wtype == 0) {
+      const size_t nw = wa::wv_pack_words(m->cfg.n_text_head, Dt);
+      L.cv_p = m->dev.alloc<uint32_t>(nw);
+      if (!L.cv_p || wa::launch_wv_pack(L.cv_raw, m->cfg.n_text_head, Dt, L.cv_p, nullptr) != hipSuccess)
+        return fail(WQ4_ENOMEM, "cross-attention Wv repack");
+      m->bytes += nw * 4;
+    }
     L.cv_b = B.bias_cat({p + ".cross_attn.value.bias"}, Dt);
     L.cout = B.q4({p + ".cross_attn.out.weight"}, {Dt}, Dt);
     L.cout_b = B.vec(p + ".cross_attn.out.bias", Dt, -0.02f, 0.02f);
@@ -833,7 +841,7 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
       WA_WQ4(wq4_layernorm(g.xd, L.ln2_w, L.ln2_b, rows, D, m->prec, g.atd_dec, nullptr, st));
       WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, g.atd_dec, nullptr, g.qd, nullptr, rows, 0u, m->prec, 2, st));
     }
-    WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_b, m->wtype, enc, B, Tq, T, H, D, g.xqt, g.xattn_part,
+    WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, Tq, T, H, D, g.xqt, g.xattn_part,
                             g.atd_dec, m->ns, st));
     if (fold) {
       const wq4_ln_fold prod3{L.ln3_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
@@ -1351,11 +1359,11 @@ wq4_status wa_probe_kernels(wa_model* m, int n_clips, int iters, double* out) {
   WA_HIP(hipEventCreate(&b));
   float ms = 0.0f;
   // cross-attention of one decode step (Tq = 1): streams every clip's encoder output
-  WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_b, m->wtype, enc, B, 1, T, H, D, g.xqt, g.xattn_part,
+  WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, 1, T, H, D, g.xqt, g.xattn_part,
                           g.atd_dec, m->ns, st));
   WA_HIP(hipEventRecord(a, st));
   for (int i = 0; i < iters; ++i)
-    WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_b, m->wtype, enc, B, 1, T, H, D, g.xqt, g.xattn_part,
+    WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, 1, T, H, D, g.xqt, g.xattn_part,
                             g.atd_dec, m->ns, st));
   WA_HIP(hipEventRecord(b, st));
   WA_HIP(hipEventSynchronize(b));
@@ -1401,8 +1409,14 @@ wq4_status wa_xattn_check(int device, const float* q_dev, const uint8_t* wk_dev,
   WA_HIP(hipMemset(qt, 0, (size_t)R * ns * HP * D * 2));
   WA_HIP(hipMemset(tiled, 0, tb));
   WA_HIP(wa::launch_enc_planes(enc_dev, (int64_t)n_clips * T, D, ns, planes, nullptr));
-  WA_HIP(wa::launch_xattn(q_dev, wk_dev, wv_dev, bv_dev, weight_type, planes, n_clips, Tq, T, H, D, qt, part, tiled,
-                          ns, nullptr));
+  uint32_t* wvp = nullptr;
+  if (weight_type == 0) {
+    wvp = d.alloc<uint32_t>(wa::wv_pack_words(H, D));
+    if (!wvp) return fail(WQ4_ENOMEM, "allocation failed");
+    WA_HIP(wa::launch_wv_pack(wv_dev, H, D, wvp, nullptr));
+  }
+  WA_HIP(wa::launch_xattn(q_dev, wk_dev, wv_dev, wvp, bv_dev, weight_type, planes, n_clips, Tq, T, H, D, qt, part,
+                          tiled, ns, nullptr));
   WA_HIP(wa::launch_untile(tiled, R, D, ns, out_dev, nullptr));
   WA_HIP(hipDeviceSynchronize());
   return WQ4_OK;

@@ -487,6 +487,37 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   }
 }
 
+// Wv (Q4_0) repacked once at model load into the projection's lane order,
+// the same bytes as the Q4 blocks: per (head, block kb, m-tile) one u32 per
+// lane -- lane l = (n = l & 15, lq = l >> 4) gets the nibbles of elements
+// 8 lq .. + 7 of weight row 16 m-tile + n, element 2i in bits 8i .. 8i + 3,
+// 2i + 1 in bits 8i + 4 .. 8i + 7 -- then the 16 rows' f16 scales:
+// [h][kb][m-tile][64 u32 | 16 u16].  xattn_out loads them straight into
+// registers: no LDS stage, no per-launch byte shuffling.
+constexpr int kWvPackU32 = 64 + 8;  // u32 words per (h, kb, m-tile)
+__global__ __launch_bounds__(256) void wv_pack_kernel(const uint8_t* __restrict__ wv, int H, int D,
+                                                      uint32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int nkb = D / 32;
+  if (i >= (int64_t)H * nkb * 4 * 64) return;
+  const int l = (int)(i & 63), mt = (int)((i >> 6) & 3);
+  const int64_t hk = i >> 8;
+  const int kb = (int)(hk % nkb), h = (int)(hk / nkb);
+  const int n = l & 15, lq = l >> 4;
+  const uint8_t* blk = wv + ((size_t)h * 64 + mt * 16 + n) * ((size_t)nkb * 18) + (size_t)kb * 18;
+  // element e of the block: low nibble of byte 2 + e (e < 16), else high nibble of byte 2 + e - 16
+  uint32_t wd = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int e = 8 * lq + j;
+    const uint32_t q = e < 16 ? (blk[2 + e] & 15u) : (blk[2 + e - 16] >> 4);
+    wd |= q << (4 * j);
+  }
+  uint32_t* o = out + (((size_t)h * nkb + kb) * 4 + mt) * kWvPackU32;
+  o[l] = wd;
+  if (lq == 0) reinterpret_cast<uint16_t*>(o + 64)[n] = (uint16_t)(blk[0] | (blk[1] << 8));
+}
+
 // ---------------------------------------- merge + out = Wv Zn + bv --
 // grid (H, ceil(R / RPW)), 512 threads: the head's 64 raw Wv rows (46 KB of
 // Q4_0 blocks, LDS-DMA) and RPW rows of Zn in LDS.  Q4 weights: the
@@ -503,9 +534,8 @@ template <int NS, int WK, int RPW, int SM, int MTG>
 __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict__ zpart,
                                                         const float* __restrict__ mlpart, int R, int H, int D, int S,
                                                         const uint8_t* __restrict__ wv,
+                                                        const uint32_t* __restrict__ wvp,
                                                         const float* __restrict__ bv, _Float16* __restrict__ tiled) {
-  constexpr int kStage = WK == kWtQ4 ? 64 * (kMaxD / 32) * 18 : 16;  // 46 KB of Q4 blocks
-  __shared__ __attribute__((aligned(16))) uint8_t sw[kStage];
   // Zn of the RPW rows: f32 [column][row] (f16 weights, VALU projection) or
   // f16 hi / lo planes [row][column] (Q4 weights, MFMA projection)
   constexpr int ZLD = kMaxD + 8;  // halves; == 4 dwords (mod 64): conflict-free B fragment reads
@@ -522,15 +552,22 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
   const int nkb = D / 32;
   // the value bias of this thread's final outputs, loaded up front
   const float bias1 = tid < 16 * NMT * RPW ? bv[h * 64 + 16 * mt0 + (tid & (16 * NMT - 1))] : 0.0f;
-  const size_t rowbytes = (size_t)nkb * 18;
-  if (WK == kWtQ4) {  // the head's 64 rows are contiguous: 64 * nkb * 18 bytes
-    const uint8_t* src = wv + ((size_t)h * 64 + 16 * mt0) * rowbytes;
-    // LDS-DMA (global_load_lds_dwordx4): 1 KiB pieces straight into the
-    // stage, every piece of a wave in flight at once (64 * 720 B = 45 KiB)
-    const int nbytes = (int)(16 * NMT * rowbytes);  // a multiple of 16 (16 * 18 * D / 32)
-    const int w = tid >> 6, lane = tid & 63;
-    for (int pc = w; pc * 1024 < nbytes && WA_XATTN_ODIAG != 1; pc += 8)
-      if (pc * 1024 + lane * 16 < nbytes) wq4::glds16(src + (size_t)pc * 1024 + lane * 16, &sw[pc * 1024]);
+  // Q4: this wave's packed nibbles and scales (blocks kb = w, w + 8, ...,
+  // its m-tiles), issued before the merge's loads: both in flight together
+  constexpr int KPW = kMaxD / 32 / 8;  // blocks per wave
+  uint32_t wq[WK == kWtQ4 ? KPW : 1][WK == kWtQ4 ? NMT : 1], wd[WK == kWtQ4 ? KPW : 1][WK == kWtQ4 ? NMT : 1];
+  if constexpr (WK == kWtQ4) {
+    const int l = tid & 63, w = tid >> 6;
+#pragma unroll
+    for (int u = 0; u < KPW; ++u) {
+      const int kb = w + 8 * u < nkb ? w + 8 * u : 0;
+#pragma unroll
+      for (int mt = 0; mt < NMT; ++mt) {
+        const uint32_t* o = wvp + (((size_t)h * nkb + kb) * 4 + mt0 + mt) * kWvPackU32;
+        wq[u][mt] = WA_XATTN_ODIAG == 1 ? 0u : o[l];
+        wd[u][mt] = WA_XATTN_ODIAG == 1 ? 0u : reinterpret_cast<const uint16_t*>(o + 64)[l & 15];
+      }
+    }
   }
   // merge of the S frame ranges (flash-attention merge, fixed split order):
   // Zn[c] = (sum_s w_s Z_s[c]) / (sum_s w_s L_s), w_s = exp(M_s - max_s M_s).
@@ -596,7 +633,6 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
     }
   }
   if (tid < 8) zzero[tid] = (_Float16)0.0f;
-  if (WK == kWtQ4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stage pieces landed
   __syncthreads();
   constexpr int NPART = WK == kWtQ4 ? 8 : 16;  // partials per output in red
   if constexpr (WK == kWtQ4) {
@@ -608,26 +644,27 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
     // block = low (l >> 4 < 2) or high nibbles of nibble bytes 8 ((l >> 4) & 1)
     // .. + 7; B row n = l & 15, the same 8 columns.
     const int w = tid >> 6, l = tid & 63, n = l & 15, lq = l >> 4;
-    const int sh = (lq >> 1) * 4;
     floatx4 acc[4];
 #pragma unroll
     for (int mt = 0; mt < NMT; ++mt) acc[mt] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-    for (int kb = w; kb < (WA_XATTN_ODIAG == 3 ? 0 : nkb); kb += 8) {
+#pragma unroll
+    for (int u = 0; u < KPW; ++u) {
+      const int kb = w + 8 * u;
+      if (kb >= (WA_XATTN_ODIAG == 3 ? 0 : nkb)) break;
       const _Float16* zhp = n < RPW ? &zh[n * ZLD + kb * 32 + 8 * lq] : zzero;
       const _Float16* zlp = n < RPW ? &zl[n * ZLD + kb * 32 + 8 * lq] : zzero;
       const half8 bh = *reinterpret_cast<const half8*>(zhp);
       const half8 bl = *reinterpret_cast<const half8*>(zlp);
 #pragma unroll
       for (int mt = 0; mt < NMT; ++mt) {  // local m-tile: outputs 16 (mt0 + mt) ..
-        const uint16_t* blk = reinterpret_cast<const uint16_t*>(&sw[(size_t)(mt * 16 + n) * rowbytes + (size_t)kb * 18]);
-        const _Float16 d = __builtin_bit_cast(_Float16, blk[0]) * (_Float16)kWvScale;  // exact: d < 16
+        const _Float16 d = __builtin_bit_cast(_Float16, (uint16_t)wd[u][mt]) * (_Float16)kWvScale;  // exact: d < 16
         const half2v off = {(_Float16)1032.0f, (_Float16)1032.0f};
         const half2v dv = {d, d};
         half8 ah, al;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const uint32_t x = (uint32_t)blk[1 + 4 * (lq & 1) + i] >> sh;
-          const uint32_t pr = (x & 0xFu) | ((x << 8) & 0xF0000u) | 0x64006400u;
+          const uint32_t x = wq[u][mt] >> (8 * i);  // elements 2i, 2i + 1 in its low two nibbles
+          const uint32_t pr = (x & 0xFu) | ((x << 12) & 0xF0000u) | 0x64006400u;
           const half2v qv = __builtin_bit_cast(half2v, pr) - off;  // exact q - 8
           const half2v hv = qv * dv;
           const half2v lv = __builtin_elementwise_fma(qv, dv, -hv);  // exact remainder
@@ -969,27 +1006,27 @@ int out_rows(int R) {
   return WA_XATTN_OUT_ROWS;
 }
 template <int NS, int WK, int RPW>
-void launch_out_rpw(int R, int H, const float* z, const float* ml, int D, int S, const uint8_t* wv, const float* bv,
-                    _Float16* tiled, hipStream_t st, bool split_outputs) {
+void launch_out_rpw(int R, int H, const float* z, const float* ml, int D, int S, const uint8_t* wv,
+                    const uint32_t* wvp, const float* bv, _Float16* tiled, hipStream_t st, bool split_outputs) {
   const dim3 go(H, (R + RPW - 1) / RPW);
   if constexpr (WK == kWtQ4) {
     if (split_outputs) {  // few rows: 4 workgroups per head
       hipLaunchKernelGGL((xattn_out_kernel<NS, WK, RPW, kXattnSplits, 4>), dim3(go.x, go.y, 4), dim3(512), 0, st, z,
-                         ml, R, H, D, S, wv, bv, tiled);
+                         ml, R, H, D, S, wv, wvp, bv, tiled);
       return;
     }
   }
   hipLaunchKernelGGL((xattn_out_kernel<NS, WK, RPW, kXattnSplits, 1>), go, dim3(512), 0, st, z, ml, R, H, D, S, wv,
-                     bv, tiled);
+                     wvp, bv, tiled);
 }
 template <int NS, int WK>
-void launch_out(int R, int H, const float* z, const float* ml, int D, int S, const uint8_t* wv, const float* bv,
-                _Float16* tiled, hipStream_t st, bool split_outputs = false) {
+void launch_out(int R, int H, const float* z, const float* ml, int D, int S, const uint8_t* wv, const uint32_t* wvp,
+                const float* bv, _Float16* tiled, hipStream_t st, bool split_outputs = false) {
   switch (out_rows(R)) {
-    case 1: launch_out_rpw<NS, WK, 1>(R, H, z, ml, D, S, wv, bv, tiled, st, split_outputs); break;
-    case 2: launch_out_rpw<NS, WK, 2>(R, H, z, ml, D, S, wv, bv, tiled, st, split_outputs); break;
-    case 8: launch_out_rpw<NS, WK, 8>(R, H, z, ml, D, S, wv, bv, tiled, st, split_outputs); break;
-    default: launch_out_rpw<NS, WK, 4>(R, H, z, ml, D, S, wv, bv, tiled, st, split_outputs); break;
+    case 1: launch_out_rpw<NS, WK, 1>(R, H, z, ml, D, S, wv, wvp, bv, tiled, st, split_outputs); break;
+    case 2: launch_out_rpw<NS, WK, 2>(R, H, z, ml, D, S, wv, wvp, bv, tiled, st, split_outputs); break;
+    case 8: launch_out_rpw<NS, WK, 8>(R, H, z, ml, D, S, wv, wvp, bv, tiled, st, split_outputs); break;
+    default: launch_out_rpw<NS, WK, 4>(R, H, z, ml, D, S, wv, wvp, bv, tiled, st, split_outputs); break;
   }
 }
 
@@ -1037,12 +1074,22 @@ hipError_t launch_enc_planes(const float* x, int64_t rows, int D, int ns, _Float
   return hipGetLastError();
 }
 
-hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, const float* bv, int wtype,
-                        const _Float16* enc, int B, int Tq, int T, int H, int D, _Float16* qt, float* part,
+size_t wv_pack_words(int H, int D) { return (size_t)H * (D / 32) * 4 * kWvPackU32; }
+
+hipError_t launch_wv_pack(const uint8_t* wv, int H, int D, uint32_t* out, hipStream_t st) {
+  if (D % 32 != 0 || D > kMaxD) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)H * (D / 32) * 4 * 64;
+  hipLaunchKernelGGL(wv_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, wv, H, D, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, const uint32_t* wvp, const float* bv,
+                        int wtype, const _Float16* enc, int B, int Tq, int T, int H, int D, _Float16* qt, float* part,
                         _Float16* tiled, int ns, hipStream_t st) {
   const int R = B * Tq;
   const int HT = (H + 15) / 16, HP = HT * 16;
   if (D != H * 64 || D % 128 != 0 || D > kMaxD || H > 20) return hipErrorInvalidValue;
+  if (wtype == kWtQ4 && !wvp) return hipErrorInvalidValue;  // Q4: the load-time packed Wv (launch_wv_pack)
   const XattnPlan p = xattn_plan(R, T);
   float* z = part;
   float* ml = part + (size_t)R * p.splits * H * D;
@@ -1081,14 +1128,14 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   // merge the splits and project with Wv into the output projection's operand
   if (wtype == kWtQ4) {
     if (ns == 2)
-      launch_out<2, kWtQ4>(R, H, z, ml, D, p.splits, wv, bv, tiled, st, small);
+      launch_out<2, kWtQ4>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, st, small);
     else
-      launch_out<1, kWtQ4>(R, H, z, ml, D, p.splits, wv, bv, tiled, st, small);
+      launch_out<1, kWtQ4>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, st, small);
   } else {
     if (ns == 2)
-      launch_out<2, kWtF16>(R, H, z, ml, D, p.splits, wv, bv, tiled, st, small);
+      launch_out<2, kWtF16>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, st, small);
     else
-      launch_out<1, kWtF16>(R, H, z, ml, D, p.splits, wv, bv, tiled, st, small);
+      launch_out<1, kWtF16>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, st, small);
   }
   return hipGetLastError();
 }

@@ -63,6 +63,9 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill_float, dim3(blocks(D)), dim3(256), 0, 0, bv, (size_t)D, 0.1f);
   hipLaunchKernelGGL(fill_q4, dim3(blocks(wbytes / 18)), dim3(256), 0, 0, wk, wbytes / 18);
   hipLaunchKernelGGL(fill_q4, dim3(blocks(wbytes / 18)), dim3(256), 0, 0, wv, wbytes / 18);
+  uint32_t* wvp;
+  CK(hipMalloc(&wvp, wa::wv_pack_words(H, D) * 4));
+  CK(wa::launch_wv_pack(wv, H, D, wvp, 0));
   CK(hipDeviceSynchronize());
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
@@ -89,14 +92,14 @@ int main(int argc, char** argv) {
                          q, R, D, wk, HP, qt);
     });
     const float t_out = time_it([&] {
-      wa::launch_out<2, wa::kWtQ4>(R, H, z, ml, D, p.splits, wv, bv, tiled, 0);
+      wa::launch_out<2, wa::kWtQ4>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, 0);
     });
     const float t_out4 = time_it([&] {
-      wa::launch_out<2, wa::kWtQ4>(R, H, z, ml, D, p.splits, wv, bv, tiled, 0, true);
+      wa::launch_out<2, wa::kWtQ4>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, 0, true);
     });
     printf("{\"rows\": %d, \"out_split4_us\": %.2f}\n", R, t_out4);
     const float t_all = time_it([&] {
-      wa::launch_xattn(q, wk, wv, bv, wa::kWtQ4, enc, R, 1, T, H, D, qt, part, tiled, NS, 0);
+      wa::launch_xattn(q, wk, wv, wvp, bv, wa::kWtQ4, enc, R, 1, T, H, D, qt, part, tiled, NS, 0);
     });
     float t_sc = 0.0f, t_z = 0.0f;
     if (R <= wa::kSmallRowsMax) {  // the split phases one by one
