@@ -87,6 +87,19 @@ void wq4_tensor_destroy(wq4_tensor* t);
  * two MFMA passes instead of three).  dequantize() returns the f16 values
  * as f32; raw_bytes() the 2*N*K bytes as given. */
 wq4_status wq4_tensor_create_f16(int device, const uint16_t* w, int64_t n, int64_t k, wq4_tensor** out);
+/* Creation flags of the _ex forms.  By default a tensor with K % 128 == 0
+ * and N % 16 == 0 also gets the decode-step (<= 32 rows) kernel's weight
+ * layout, a second device copy of the weights; WQ4_TENSOR_NO_DECODE_STEP
+ * skips it for tensors that never run at <= 32 rows (encoder weights), and
+ * such tensors use the other kernels at every row count. */
+#define WQ4_TENSOR_NO_DECODE_STEP 1u
+wq4_status wq4_tensor_create_ex(int device, const uint8_t* raw, size_t nbytes, int64_t n, int64_t k, unsigned flags,
+                                wq4_tensor** out);
+wq4_status wq4_tensor_create_f16_ex(int device, const uint16_t* w, int64_t n, int64_t k, unsigned flags,
+                                    wq4_tensor** out);
+/* 1 if the tensor holds the decode-step kernel's layout (see above; for f16
+ * weights also only when max |w| * 256 stays finite in f16). */
+int wq4_tensor_has_decode_step(const wq4_tensor* t);
 /* 0 = Q4_0 blocks, 1 = f16 weights. */
 int wq4_tensor_weight_type(const wq4_tensor* t);
 /* Q4Tensor::shape (tensor.rs:74-76): [N, K]. */

@@ -163,10 +163,12 @@ def test_decode_group_rows():
         assert whisper_amd.decode_group_rows(n) == want, n
 
 
-def test_bench_in_graph_lookup(tmp_path, monkeypatch):
+@pytest.mark.parametrize("heads,d_model", [(20, 1280), (16, 1024)])
+def test_bench_in_graph_lookup(tmp_path, monkeypatch, heads, d_model):
     """bench.in_graph_xattn sums the three cross-attention kernels at the
     group's grids from profiles/xattn_in_graph.json, only for the same
-    workload."""
+    workload; grids follow the head count and width (Large-V3 H = 20,
+    Medium H = 16)."""
     import json
     import sys
 
@@ -175,12 +177,14 @@ def test_bench_in_graph_lookup(tmp_path, monkeypatch):
 
     wl = {"variant": "large_v3", "weights": "q4_0", "precision": "f16x2", "clips": 32}
     (tmp_path / "profiles").mkdir()
-    rows = [{"kernel": "xattn_q_mfma_kernel", "grid": [2560, 20, 1], "avg_us": 5.5},
+    rows = [{"kernel": "xattn_q_mfma_kernel", "grid": [heads * 128, d_model // 64, 1], "avg_us": 5.5},
             {"kernel": "xattn_main_kernel", "grid": [4096, 16, 1], "avg_us": 38.0},
             {"kernel": "xattn_main_kernel", "grid": [4096, 32, 1], "avg_us": 48.0},
-            {"kernel": "xattn_out_kernel", "grid": [10240, 4, 1], "avg_us": 12.5}]
+            {"kernel": "xattn_out_kernel", "grid": [heads * 512, 4, 1], "avg_us": 12.5}]
     (tmp_path / "profiles" / "xattn_in_graph.json").write_text(json.dumps({"workload": wl, "kernels": rows}))
     monkeypatch.setattr(bench, "REPO", str(tmp_path))
-    assert bench.in_graph_xattn(16, 20, 1280, wl) == 5.5 + 38.0 + 12.5
-    assert bench.in_graph_xattn(16, 20, 1280, dict(wl, clips=16)) is None
-    assert bench.in_graph_xattn(8, 20, 1280, wl) is None  # no trace at that grid
+    assert bench.in_graph_xattn(16, heads, d_model, wl) == 5.5 + 38.0 + 12.5
+    assert bench.in_graph_xattn(16, heads, d_model, dict(wl, clips=16)) is None
+    assert bench.in_graph_xattn(8, heads, d_model, wl) is None  # no trace at that grid
+    other = (16, 1024) if heads == 20 else (20, 1280)
+    assert bench.in_graph_xattn(16, other[0], other[1], wl) is None  # another model's grids

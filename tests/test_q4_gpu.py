@@ -580,3 +580,117 @@ def test_ln_fold_matches_layernorm_path(torch, wtype, prec, m, n2, flags, kern):
     for zz in (z_ref, z):
         err = np.abs(zz.cpu().numpy() - z64)
         assert np.all(err <= c * scale + 1e-6), float(np.max(err / (scale + 1e-30)))
+
+
+# ------------------------------------------- range and layout edge cases --
+@pytest.mark.parametrize("policy", [1, 2, 3])
+def test_ffn_large_range_vs_oracle(torch, policy):
+    """Q4FFN with inputs around 1e3-1e4 and fc1 outputs far beyond the
+    internal operands' 2^4-scaled f16 range (|gelu(fc1 x)| up to ~1e6): each
+    GEMM's operand scale comes from its own input's max |x|, so the result
+    stays finite and within the f16x2 tolerance of the float64 oracle (the
+    reference's f32 path has no range limit below FLT_MAX)."""
+    wq4.set_kernel_policy(policy)
+    d, f, m = 256, 1024, 32 if policy == 3 else 40
+    rng = np.random.default_rng(77)
+    q1 = oracle.quantize_convert_np((rng.standard_normal(f * d) * 0.5).astype(np.float32))
+    q2 = oracle.quantize_convert_np((rng.standard_normal(d * f) * 0.05).astype(np.float32))
+    b1 = (rng.standard_normal(f) * 10).astype(np.float32)
+    b2 = (rng.standard_normal(d) * 0.01).astype(np.float32)
+    x = (rng.standard_normal(m * d) * 3e3).astype(np.float32)
+    x[::7] *= 3.0  # some |x| ~ 1e4
+    ffn = wq4.Q4FFN(wq4.Q4Linear(wq4.Q4Tensor.from_q4_bytes(q1, [f, d]), to_dev(torch, b1, (f,))),
+                    wq4.Q4Linear(wq4.Q4Tensor.from_q4_bytes(q2, [d, f]), to_dev(torch, b2, (d,))))
+    y = ffn.forward(to_dev(torch, x, (1, m, d))).cpu().numpy().reshape(m, d)
+    assert np.all(np.isfinite(y))
+    w1 = oracle.dequantize_np(q1, f * d).reshape(f, d).astype(np.float64)
+    w2 = oracle.dequantize_np(q2, d * f).reshape(d, f).astype(np.float64)
+    h = x.reshape(m, d).astype(np.float64) @ w1.T + b1
+    assert np.max(np.abs(h)) > 4094.0 * 4, "the test must exceed the old fixed operand range"
+    g = oracle.gelu_np(h.astype(np.float32)).astype(np.float64)
+    want = g @ w2.T + b2
+    mag = np.abs(g) @ np.abs(w2).T + 1.0
+    assert np.max(np.abs(y - want) / mag) < 2e-5
+
+
+@pytest.mark.parametrize("kern", [3, 2])
+def test_ln_fold_producer_statistics_n1312(torch, kern):
+    """LayerNorm-fold producer at N = 1312 (N % 64 == 32: the last 64-column
+    slab of the decode-step kernel is half padding): the 16-column tile
+    statistics land in exactly rows * N / 16 slots -- a poisoned guard region
+    right after them stays untouched -- and equal (mean, M2) of each tile of
+    the produced x."""
+    import ctypes
+
+    n, k, m = 1312, 1280, 13
+    rng = np.random.default_rng(1312 + kern)
+    w = wq4.Q4Tensor.from_q4_bytes(oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.05).astype(np.float32)),
+                                   [n, k])
+    L = wq4.lib()
+    wq4.set_kernel_policy(kern)
+    if L.wq4_lnfold_supported(w.handle, m) != 1:
+        pytest.skip("no LayerNorm-fold kernel for this shape under this policy")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    a = to_dev(torch, rng.standard_normal(m * k).astype(np.float32), (m, k))
+    at_a = torch.zeros(L.wq4_atiled_bytes(m, k, 0), dtype=torch.uint8, device="cuda:0")
+    wq4.check(L.wq4_tile_activations(p(a), m, k, k, 0, p(at_a), at_a.numel(), st))
+    res = to_dev(torch, rng.standard_normal(m * n).astype(np.float32), (m, n))
+    b = to_dev(torch, (rng.standard_normal(n) * 0.1).astype(np.float32), (n,))
+    gam = to_dev(torch, rng.uniform(0.8, 1.2, n).astype(np.float32), (n,))
+    x_ref = res.clone()
+    wq4.check(L.wq4_gemm_tiled(w.handle, p(b), p(at_a), p(x_ref), p(x_ref), None, m, 2, 0, kern, st))
+    nslots = m * (n // 16) * 2
+    stats = torch.full((nslots + 4096,), 12345.0, device="cuda:0")
+    at_f = torch.zeros(L.wq4_atiled_bytes(m, n, 0), dtype=torch.uint8, device="cuda:0")
+    x = res.clone()
+    prod = wq4.LnFold(gam.data_ptr(), at_f.data_ptr(), stats.data_ptr(), None, None)
+    wq4.check(L.wq4_gemm_tiled_lnfold(w.handle, p(b), p(at_a), p(x), p(x), None, m, 2, 0, ctypes.byref(prod), st))
+    torch.cuda.synchronize()
+    xs = x.cpu().numpy()
+    assert np.array_equal(xs.view(np.uint32), x_ref.cpu().numpy().view(np.uint32))
+    s = stats.cpu().numpy()
+    assert np.all(s[nslots:] == 12345.0), "statistics written past rows * N / 16 slots"
+    got = s[:nslots].reshape(m, n // 16, 2)
+    tiles = xs.astype(np.float64).reshape(m, n // 16, 16)
+    mean = tiles.mean(axis=2)
+    m2 = ((tiles - mean[..., None]) ** 2).sum(axis=2)
+    assert np.allclose(got[..., 0], mean, rtol=1e-5, atol=1e-5)
+    assert np.allclose(got[..., 1], m2, rtol=1e-4, atol=1e-4)
+
+
+def test_tensor_without_decode_step_layout(torch):
+    """WQ4_TENSOR_NO_DECODE_STEP (encoder weights): no second weight copy,
+    and <= 32-row calls fall back to the other kernels within tolerance."""
+    n, k, m = 1280, 1280, 8
+    rng = np.random.default_rng(5)
+    q = oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.05).astype(np.float32))
+    deq = oracle.dequantize_np(q, n * k).reshape(n, k)
+    full = wq4.Q4Tensor.from_q4_bytes(q, [n, k])
+    lean = wq4.Q4Tensor.from_q4_bytes(q, [n, k], decode_step=False)
+    assert full.has_decode_step and not lean.has_decode_step
+    assert lean.device_bytes() < full.device_bytes()
+    assert np.array_equal(lean.raw_bytes(), q)
+    x = rng.standard_normal(m * k).astype(np.float32)
+    for policy in (0, 3):
+        wq4.set_kernel_policy(policy)
+        y = wq4.q4_matmul(to_dev(torch, x, (1, m, k)), lean).cpu().numpy().reshape(m, n)
+        assert_q4_close(y, x.reshape(m, k), deq, what=f"no decode-step layout, policy {policy}")
+
+
+def test_f16_weights_out_of_decode_step_range(torch):
+    """f16 weights with |w| >= 256 (w * 2^8 would overflow the decode-step
+    kernel's f16 layout): that layout is not built and small-row GEMMs use
+    the other kernels, still within the f16x2 tolerance."""
+    n, k, m = 256, 512, 4
+    rng = np.random.default_rng(6)
+    w = (rng.standard_normal((n, k)) * 0.03).astype(np.float16)
+    w[3, 17] = np.float16(300.0)
+    t = wq4.Q4Tensor.from_f16(w)
+    assert not t.has_decode_step
+    x = rng.standard_normal(m * k).astype(np.float32)
+    for policy in (0, 3):
+        wq4.set_kernel_policy(policy)
+        y = wq4.q4_matmul(to_dev(torch, x, (1, m, k)), t).cpu().numpy().reshape(m, n)
+        assert np.all(np.isfinite(y))
+        assert_q4_close(y, x.reshape(m, k), w.astype(np.float32), what=f"f16 |w| >= 256, policy {policy}")

@@ -214,7 +214,7 @@ struct wa_model {
   std::vector<DecGroup> groups;
   int wtype = 0;     // linear weights: 0 Q4_0, 1 f16 (BASELINE config 5)
   int kv_batch = 0;  // clips of the last encoder pass (enc_planes valid for [0, kv_batch))
-  hipStream_t own_stream = nullptr;  // encoder / cross-K/V (graph capture needs a non-null stream)
+  hipStream_t own_stream = nullptr;  // encoder / encoder planes (graph capture needs a non-null stream)
   float timings[5] = {0, 0, 0, 0, 0};
   // decode-step logit trace (wa_transcribe_trace; null otherwise): device
   // [clip][trace_s1][trace_k] ids and their logits
@@ -387,7 +387,10 @@ struct Builder {
   float* vec(const std::string& name, int64_t n, float lo, float hi) { return upload(get(name, n, lo, hi)); }
   // Linear weights of several GGUF tensors [n_i, k], row-concatenated (a
   // fused projection): Q4_0 blocks, or f16 halves for an F16 model.
-  wq4_tensor* q4(const std::vector<std::string>& names, const std::vector<int>& rows, int k) {
+  // decode_step = false: the tensor never runs at <= 32 rows (encoder), so
+  // the decode-step kernel's second weight copy is not built.
+  wq4_tensor* q4(const std::vector<std::string>& names, const std::vector<int>& rows, int k, bool decode_step = true) {
+    const unsigned cflags = decode_step ? 0u : WQ4_TENSOR_NO_DECODE_STEP;
     if (st != WQ4_OK) return nullptr;
     int64_t total = 0;
     for (int r : rows) total += r;
@@ -402,7 +405,7 @@ struct Builder {
         off += (size_t)rows[i] * k;
       }
       wq4_tensor* t = nullptr;
-      wq4_status s = wq4_tensor_create_f16(m->device, h.data(), total, k, &t);
+      wq4_status s = wq4_tensor_create_f16_ex(m->device, h.data(), total, k, cflags, &t);
       if (s != WQ4_OK) st = fail(s, std::string("F16 weight upload: ") + wq4_last_error());
       m->bytes += wq4_tensor_device_bytes(t);
       return t;
@@ -417,7 +420,7 @@ struct Builder {
       off += (size_t)rows[i] * k / 32 * 18;
     }
     wq4_tensor* t = nullptr;
-    wq4_status s = wq4_tensor_create(m->device, raw.data(), raw.size(), total, k, &t);
+    wq4_status s = wq4_tensor_create_ex(m->device, raw.data(), raw.size(), total, k, cflags, &t);
     if (s != WQ4_OK) st = fail(s, std::string("Q4 upload: ") + wq4_last_error());
     m->bytes += wq4_tensor_device_bytes(t);
     return t;
@@ -484,15 +487,15 @@ wq4_status build_model(wa_model* m, Source& src) {
     EncLayer& L = m->enc[i];
     L.ln1_w = B.vec(p + ".attn_ln.weight", D, 0.9f, 1.1f);
     L.ln1_b = B.vec(p + ".attn_ln.bias", D, -0.05f, 0.05f);
-    L.qkv = B.q4({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, {D, D, D}, D);
+    L.qkv = B.q4({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, {D, D, D}, D, false);
     L.qkv_b = B.bias_cat({p + ".attn.query.bias", p + ".attn.key.bias", p + ".attn.value.bias"}, D);
-    L.out = B.q4({p + ".attn.out.weight"}, {D}, D);
+    L.out = B.q4({p + ".attn.out.weight"}, {D}, D, false);
     L.out_b = B.vec(p + ".attn.out.bias", D, -0.02f, 0.02f);
     L.ln2_w = B.vec(p + ".mlp_ln.weight", D, 0.9f, 1.1f);
     L.ln2_b = B.vec(p + ".mlp_ln.bias", D, -0.05f, 0.05f);
-    L.fc1 = B.q4({p + ".mlp.0.weight"}, {F}, D);
+    L.fc1 = B.q4({p + ".mlp.0.weight"}, {F}, D, false);
     L.fc1_b = B.vec(p + ".mlp.0.bias", F, -0.02f, 0.02f);
-    L.fc2 = B.q4({p + ".mlp.2.weight"}, {D}, F);
+    L.fc2 = B.q4({p + ".mlp.2.weight"}, {D}, F, false);
     L.fc2_b = B.vec(p + ".mlp.2.bias", D, -0.02f, 0.02f);
     if (B.st != WQ4_OK) return B.st;
   }
@@ -798,7 +801,7 @@ bool fused_pick(const DecGroup& g, int Tq, const wa::DecodeState* state) {
 
 // Decoder pass over Tq new tokens for the clips of group g (forward_prompt
 // when state == nullptr, decode_step otherwise), ending in last-position
-// logits.  Self-KV and cross-K/V are addressed at the group's clip offset.
+// logits.  Self-KV and the encoder planes are addressed at the group's clip offset.
 wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, const wa::DecodeState* state,
                            int pos0, int kv0, hipStream_t st) {
   const Config& c = m->cfg;
@@ -1204,7 +1207,7 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
   WA_HIP(hipEventRecord(ev[2], st));
 
   // decode groups: contiguous clip ranges on their own streams, started
-  // after the cross-K/V pass, joined back into `st` at the end
+  // after the encoder-planes pass, joined back into `st` at the end
   const int G = decode_groups(B);
   hipEvent_t kv_ready, gdone[kMaxGroups], gprompt[kMaxGroups];
   WA_HIP(hipEventCreateWithFlags(&kv_ready, hipEventDisableTiming));
@@ -1299,7 +1302,7 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
     std::memcpy(tokens_out + (size_t)b * max_tokens, tok.data() + (size_t)b * kMaxTokens,
                 (size_t)max_tokens * 4);
   }
-  // phases: encoder, cross-K/V, prompt (slowest group), decode loop
+  // phases: encoder, encoder planes (the cross-attention state), prompt (slowest group), decode loop
   float ms[3], tp = 0.0f, tall = 0.0f;
   for (int i = 0; i < 2; ++i) WA_HIP(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
   for (int i = 0; i < G; ++i) {

@@ -112,7 +112,7 @@ wq4_status decode_ws_get(int dev, void* stream, const wq4::DecodeWs** out) {
                   "workspace)");
     wq4::DecodeWs ws{nullptr, nullptr, nullptr};
     hipError_t e = hipMalloc(&ws.part, (size_t)wq4::kDecodeWsFloats * sizeof(float));
-    if (e == hipSuccess) e = hipMalloc(&ws.act_scale, 16);
+    if (e == hipSuccess) e = hipMalloc(&ws.act_scale, 32);  // two [scale, 1/scale, max bits] slots
     if (e == hipSuccess) e = hipMalloc(&ws.counters, (size_t)wq4::kDecodeMaxTiles * sizeof(int));
     if (e == hipSuccess)
       e = hipMemsetAsync(ws.counters, 0, (size_t)wq4::kDecodeMaxTiles * sizeof(int),
@@ -251,6 +251,11 @@ wq4_status wq4_set_kernel_policy(int policy) {
 // Q4Tensor::from_q4_bytes, src/gguf/tensor.rs:35-71.
 wq4_status wq4_tensor_create(int device, const uint8_t* raw, size_t nbytes, int64_t n, int64_t k,
                              wq4_tensor** out) {
+  return wq4_tensor_create_ex(device, raw, nbytes, n, k, 0u, out);
+}
+
+wq4_status wq4_tensor_create_ex(int device, const uint8_t* raw, size_t nbytes, int64_t n, int64_t k, unsigned flags,
+                                wq4_tensor** out) {
   if (!out) return fail(WQ4_EINVAL, "out is null");
   *out = nullptr;
   if (n <= 0 || k <= 0)
@@ -290,7 +295,8 @@ wq4_status wq4_tensor_create(int device, const uint8_t* raw, size_t nbytes, int6
     if (e == hipSuccess) e = hipMemcpy(t->nib, nib.data(), nib.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(t->sc, sc.data(), t->g.sc_bytes(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(t->cs, cs.data(), t->g.colscale_bytes(), hipMemcpyHostToDevice);
-    if (e == hipSuccess && k % 128 == 0 && n % 16 == 0) {  // the decode-step kernel's layout
+    if (e == hipSuccess && k % 128 == 0 && n % 16 == 0 && !(flags & WQ4_TENSOR_NO_DECODE_STEP)) {
+      // the decode-step kernel's layout
       std::vector<uint32_t> q16(wq4::skinny_q_bytes(t->g) / 4);
       std::vector<uint16_t> d16(wq4::skinny_d_bytes(t->g) / 2);
       wq4::repack_q4_skinny(raw, t->g, q16.data(), d16.data());
@@ -338,6 +344,23 @@ size_t wq4_tensor_device_bytes(const wq4_tensor* t) {
 }
 
 wq4_status wq4_tensor_create_f16(int device, const uint16_t* w, int64_t n, int64_t k, wq4_tensor** out) {
+  return wq4_tensor_create_f16_ex(device, w, n, k, 0u, out);
+}
+
+int wq4_tensor_has_decode_step(const wq4_tensor* t) { return t && t->q16 ? 1 : 0; }
+
+// The decode-step kernel keeps f16 weights as w * 2^8 (wq4_skinny.hip): only
+// when that stays finite in f16 (|w| < 255.875).
+static bool f16_skinny_in_range(const uint16_t* w, size_t count) {
+  for (size_t i = 0; i < count; ++i) {
+    const float v = std::fabs((float)__builtin_bit_cast(_Float16, w[i]));
+    if (!(v * 256.0f <= 65504.0f)) return false;  // also rejects inf / NaN
+  }
+  return true;
+}
+
+wq4_status wq4_tensor_create_f16_ex(int device, const uint16_t* w, int64_t n, int64_t k, unsigned flags,
+                                    wq4_tensor** out) {
   if (!out) return fail(WQ4_EINVAL, "out is null");
   *out = nullptr;
   if (n <= 0 || k <= 0 || k % 32 != 0)
@@ -358,7 +381,8 @@ wq4_status wq4_tensor_create_f16(int device, const uint16_t* w, int64_t n, int64
   if (e == hipSuccess) e = hipMalloc(&t->cs, t->g.colscale_bytes());
   if (e == hipSuccess) e = hipMemcpy(t->nib, frag.data(), t->g.f16_frag_bytes(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(t->cs, ones.data(), t->g.colscale_bytes(), hipMemcpyHostToDevice);
-  if (e == hipSuccess && k % 128 == 0 && n % 16 == 0) {  // the decode-step kernel's layout
+  if (e == hipSuccess && k % 128 == 0 && n % 16 == 0 && !(flags & WQ4_TENSOR_NO_DECODE_STEP) &&
+      f16_skinny_in_range(w, (size_t)(n * k))) {  // the decode-step kernel's layout
     std::vector<uint16_t> f16s(wq4::skinny_f16_bytes(t->g) / 2);
     wq4::repack_f16_skinny(w, t->g, f16s.data());
     e = hipMalloc(&t->q16, wq4::skinny_f16_bytes(t->g));
@@ -434,9 +458,15 @@ size_t wq4_linear_workspace_bytes(const wq4_tensor* w, int64_t rows) {
   return wq4::atiled_bytes(rows, w->g.k, 2);
 }
 
+// fc1's operand, fc2's operand and the f32 fc1 output between them.
+static size_t ffn_ws_bytes(const wq4_tensor* fc1, const wq4_tensor* fc2, int64_t rows, int ns) {
+  return wq4::atiled_bytes(rows, fc1->g.k, ns) + wq4::atiled_bytes(rows, fc2->g.k, ns) +
+         (size_t)rows * (size_t)fc1->g.n * sizeof(float);
+}
+
 size_t wq4_ffn_workspace_bytes(const wq4_tensor* fc1, const wq4_tensor* fc2, int64_t rows) {
-  if (!fc1 || !fc2 || fc1->flat || fc2->flat) return 0;
-  return wq4::atiled_bytes(rows, fc1->g.k, 2) + wq4::atiled_bytes(rows, fc2->g.k, 2);
+  if (!fc1 || !fc2 || fc1->flat || fc2->flat || rows < 0) return 0;
+  return ffn_ws_bytes(fc1, fc2, rows, 2);
 }
 
 static wq4_status linear_impl(const wq4_tensor* w, const float* bias, const float* x, const float* residual,
@@ -524,30 +554,41 @@ static wq4_status ffn_impl(const wq4_tensor* fc1, const float* b1, const wq4_ten
   const int ns = ns_of(prec);
   const size_t n1 = wq4::atiled_bytes(rows, fc1->g.k, ns);
   const size_t n2 = wq4::atiled_bytes(rows, fc2->g.k, ns);
-  if (!ws || ws_bytes < n1 + n2) return fail(WQ4_ENOMEM, "workspace too small: need " + std::to_string(n1 + n2));
+  const size_t need = ffn_ws_bytes(fc1, fc2, rows, ns);
+  if (!ws || ws_bytes < need) return fail(WQ4_ENOMEM, "workspace too small: need " + std::to_string(need));
   DeviceGuard dg(fc1->device);
   if (!dg.ok) return fail(WQ4_EHIP, "hipSetDevice failed");
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto* a1 = static_cast<_Float16*>(ws);
   auto* a2 = reinterpret_cast<_Float16*>(static_cast<uint8_t*>(ws) + n1);
+  auto* h = reinterpret_cast<float*>(static_cast<uint8_t*>(ws) + n1 + n2);
   const wq4::DecodeWs* dws = nullptr;
   s = decode_ws_get(fc1->device, st, &dws);
   if (s != WQ4_OK) return s;
+  // Each GEMM's A operand is scaled by a power of two picked from ITS input's
+  // max |x| (device-side, stream-ordered), so any finite f32 input and any
+  // finite gelu(fc1 x) stay finite -- the reference's f32 path has no range
+  // limit below FLT_MAX either.  fc1 + bias + GELU go to f32 first.
+  const int n1c = (int)fc1->g.n;
   hipError_t e = wq4::launch_act_scale(x, (int)rows, (int)fc1->g.k, (int)fc1->g.k, dws->act_scale, st);
   if (e == hipSuccess)
     e = wq4::launch_tile_activations(x, a1, (int)rows, (int)fc1->g.k, (int)fc1->g.k, ns, st, dws->act_scale);
   if (e != hipSuccess) return hip_fail(e, "tile_activations launch");
-  // fc1 + bias + GELU, written straight into fc2's operand layout (the fixed
-  // internal operand scale: |gelu(fc1 x)| < 4094).
-  wq4::EpiArgs e1 = make_epi(b1, nullptr, nullptr, (int)fc1->g.n, (int)rows, (int)fc1->g.n, true);
+  wq4::EpiArgs e1 = make_epi(b1, nullptr, h, n1c, (int)rows, n1c, true);
   e1.act_inv = dws->act_scale + 1;
-  e1.out_tiled = a2;
-  e1.nbp_next = (int)fc2->g.nbp;
   const int k1 = pick_kernel(fc1, rows, 0), k2 = pick_kernel(fc2, rows, 0);
-  wq4_status s1 = gemm(fc1, a1, rows, e1, wq4::kEpiTiled, ns, st, k1 == 2, k1 == 3);
+  wq4_status s1 = gemm(fc1, a1, rows, e1, wq4::kEpiF32, ns, st, k1 == 2, k1 == 3);
   if (s1 != WQ4_OK) return s1;
+  // fc2's operand scale lives in the second half of the act-scale words
+  // (fc1's may still be read by its launch: stream order keeps them apart,
+  // but a separate slot keeps the two scales independent for inspection)
+  float* sc2 = dws->act_scale + 4;
+  e = wq4::launch_act_scale(h, (int)rows, n1c, n1c, sc2, st);
+  if (e == hipSuccess) e = wq4::launch_tile_activations(h, a2, (int)rows, n1c, n1c, ns, st, sc2);
+  if (e != hipSuccess) return hip_fail(e, "tile_activations launch (fc2 operand)");
   wq4::EpiArgs e2 = make_epi(b2, (flags & WQ4_EPI_RESIDUAL) ? residual : nullptr, y, (int)fc2->g.n, (int)rows,
                              (int)fc2->g.n, (flags & WQ4_EPI_GELU) != 0);
+  e2.act_inv = sc2 + 1;
   return gemm(fc2, a2, rows, e2, wq4::kEpiF32, ns, st, k2 == 2, k2 == 3);
 }
 
@@ -570,7 +611,7 @@ wq4_status wq4_ffn_forward(const wq4_tensor* fc1, const float* b1_dev, const wq4
   const int64_t rows = b * m;
   const wq4_precision prec = wq4_get_precision();
   const int ns = ns_of(prec);
-  const size_t need = wq4::atiled_bytes(rows, fc1->g.k, ns) + wq4::atiled_bytes(rows, fc2->g.k, ns);
+  const size_t need = ffn_ws_bytes(fc1, fc2, rows, ns);
   void* ws = nullptr;
   if (rows > 0) {
     DeviceGuard dg(fc1->device);

@@ -34,7 +34,7 @@ constexpr int kDecodeMaxMTiles = 4;                     // rows <= 128 (launches
 struct DecodeWs {
   float* part;
   int* counters;
-  float* act_scale;  // [2]: the f32 entry points' per-call activation scale (launch_act_scale)
+  float* act_scale;  // [8]: the f32 entry points' per-call operand scales, two {s, 1/s, max bits} slots (launch_act_scale)
 };
 struct DecodePlan {
   int per;    // kernel instance: max block pairs per wave

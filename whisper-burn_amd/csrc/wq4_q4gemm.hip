@@ -787,7 +787,7 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
             store_tiled_slab<NS, 1>(stage, e2, mt0 + mt, nt, lane);
           } else if (wave == 1) {  // lane (row, half): the 16-column tile statistics
             const int rl = lane & 31, hf = lane >> 5, row = (mt0 + mt) * 32 + rl;
-            if (row < e.m) {
+            if (row < e.m && 2 * nt + hf < e.n / 16) {  // never a slot past N / 16
               float sum = 0.0f;
 #pragma unroll
               for (int c = 0; c < 16; ++c) sum += lnf_x[rl * 33 + 16 * hf + c];

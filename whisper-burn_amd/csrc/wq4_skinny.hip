@@ -381,7 +381,8 @@ __global__ __launch_bounds__(64 * kSkW) void skinny_gemm_kernel(const uint32_t* 
       const float mean = sum16(y[j]) * (1.0f / 16.0f);
       const float dv = y[j] - mean;
       const float m2 = sum16(dv * dv);
-      if ((ocol & 15) == 0 && o < OUT && orow < e.m)
+      // padding subtiles (N % 64 == 32: n >= N) own no statistics slot
+      if ((ocol & 15) == 0 && o < OUT && orow < e.m && n < e.n)
         *reinterpret_cast<floatx2*>(e.lnf_stats_out + ((size_t)orow * (e.n / 16) + nt * NT + (ocol >> 4)) * 2) =
             floatx2{mean, m2};
     }

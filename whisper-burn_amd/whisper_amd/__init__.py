@@ -348,7 +348,7 @@ class WhisperModel:
                 "decode_fc1": {"us": buf[2], "bytes": buf[3], "flops": buf[4]}}
 
     def encode(self, mel):
-        """encoder.rs:87-115 -> encoder_out [B, 1500, D] (also fills the cross-K/V caches)."""
+        """encoder.rs:87-115 -> encoder_out [B, 1500, D] (also writes the f16 encoder-output planes the decoder cross-attention reads)."""
         torch = _torch()
         B = mel.shape[0]
         out = torch.empty((B, self.config["n_audio_ctx"], self.config["n_audio_state"]), device=mel.device,

@@ -77,6 +77,11 @@ def _declare(L: ctypes.CDLL) -> None:
     L.wq4_debug_repack.argtypes = [u8p, c_i64, c_i64, u8p, ctypes.POINTER(ctypes.c_uint32), f32p]
     L.wq4_quantize_q4_0.argtypes = [f32p, c_i64, u8p]
     L.wq4_tensor_create_f16.argtypes = [c_int, ctypes.POINTER(ctypes.c_uint16), c_i64, c_i64, ctypes.POINTER(vp)]
+    L.wq4_tensor_create_ex.argtypes = [c_int, u8p, c_sz, c_i64, c_i64, ctypes.c_uint, ctypes.POINTER(vp)]
+    L.wq4_tensor_create_f16_ex.argtypes = [c_int, ctypes.POINTER(ctypes.c_uint16), c_i64, c_i64, ctypes.c_uint,
+                                           ctypes.POINTER(vp)]
+    L.wq4_tensor_has_decode_step.argtypes = [vp]
+    L.wq4_tensor_has_decode_step.restype = c_int
     L.wq4_tensor_weight_type.argtypes = [vp]
     L.wq4_tensor_weight_type.restype = c_int
     L.wq4_debug_unrepack.argtypes = [u8p, ctypes.POINTER(ctypes.c_uint32), f32p, c_i64, c_i64, u8p]
@@ -101,7 +106,8 @@ def _declare(L: ctypes.CDLL) -> None:
     for name in ("wq4_device_count", "wq4_set_precision", "wq4_set_kernel_policy", "wq4_tensor_create",
                  "wq4_tensor_shape", "wq4_tensor_dequantize", "wq4_tensor_raw_bytes", "wq4_matmul",
                  "wq4_linear_forward", "wq4_ffn_forward", "wq4_linear_forward_ws", "wq4_ffn_forward_ws",
-                 "wq4_debug_repack", "wq4_debug_unrepack", "wq4_debug_repacked_bytes", "wq4_quantize_q4_0", "wq4_tensor_create_f16"):
+                 "wq4_debug_repack", "wq4_debug_unrepack", "wq4_debug_repacked_bytes", "wq4_quantize_q4_0", "wq4_tensor_create_f16",
+                 "wq4_tensor_create_ex", "wq4_tensor_create_f16_ex"):
         getattr(L, name).restype = c_int
 
 
@@ -220,26 +226,33 @@ class Q4Tensor:
         self._device = device
 
     @classmethod
-    def from_q4_bytes(cls, raw_bytes, shape: Sequence[int], device: int = 0) -> "Q4Tensor":
+    def from_q4_bytes(cls, raw_bytes, shape: Sequence[int], device: int = 0,
+                      decode_step: bool = True) -> "Q4Tensor":
         """tensor.rs:35-71.  Raises WQ4Error(WQ4_ESHAPE / WQ4_EBYTES) with the
-        reference's messages on bad input."""
+        reference's messages on bad input.  decode_step=False skips the
+        <= 32-row kernel's second weight copy (WQ4_TENSOR_NO_DECODE_STEP)."""
         n, k = int(shape[0]), int(shape[1])
         raw = np.ascontiguousarray(np.frombuffer(bytes(raw_bytes), np.uint8) if isinstance(raw_bytes, (bytes, bytearray))
                                    else np.asarray(raw_bytes, np.uint8)).ravel()
         h = ctypes.c_void_p(None)
-        check(lib().wq4_tensor_create(device, _u8p(raw), raw.size, n, k, ctypes.byref(h)))
+        check(lib().wq4_tensor_create_ex(device, _u8p(raw), raw.size, n, k, 0 if decode_step else 1, ctypes.byref(h)))
         return cls(h, (n, k), device)
 
     @classmethod
-    def from_f16(cls, weights, device: int = 0) -> "Q4Tensor":
+    def from_f16(cls, weights, device: int = 0, decode_step: bool = True) -> "Q4Tensor":
         """Unquantized f16 weights [N, K] (BASELINE config 5): the same GEMM
         entry points run on them (wq4_tensor_create_f16)."""
         w = np.ascontiguousarray(np.asarray(weights), dtype=np.float16)
         n, k = w.shape
         h = ctypes.c_void_p(None)
-        check(lib().wq4_tensor_create_f16(device, w.view(np.uint16).ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)),
-                                          n, k, ctypes.byref(h)))
+        check(lib().wq4_tensor_create_f16_ex(device, w.view(np.uint16).ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)),
+                                             n, k, 0 if decode_step else 1, ctypes.byref(h)))
         return cls(h, (n, k), device)
+
+    @property
+    def has_decode_step(self) -> bool:
+        """True if the <= 32-row (decode-step) kernel's weight layout exists."""
+        return bool(lib().wq4_tensor_has_decode_step(self._h))
 
     @property
     def weight_type(self) -> str:
