@@ -276,6 +276,15 @@ wq4_status wq4_debug_repack(const uint8_t* raw, int64_t n, int64_t k, uint8_t* n
 wq4_status wq4_debug_unrepack(const uint8_t* nib, const uint32_t* sc, const float* colscale, int64_t n, int64_t k,
                               uint8_t* raw_out);
 
+/* Diagnostics: which kernel runs the encoder-size (rows > 128) Q4_0 GEMMs.
+ * 0 = the prefill tile kernel, 1 = by rows (default; WQ4_ENC_KERNEL
+ * overrides at load): the LDS-DMA ring kernel's 64 x 128 geometry while the
+ * tile kernel's grid would leave CUs idle (one clip), else the tile kernel;
+ * 2 = the ring kernel's 256 x 256 geometry, 3 = its 64 x 128 geometry,
+ * 4 = its 32 x 256 geometry.  All give bit-identical results.
+ * Returns the previous mode, -1 on a bad argument. */
+int wq4_debug_set_enc_kernel(int mode);
+
 #ifdef __cplusplus
 }
 #endif

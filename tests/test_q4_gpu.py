@@ -694,3 +694,50 @@ def test_f16_weights_out_of_decode_step_range(torch):
         y = wq4.q4_matmul(to_dev(torch, x, (1, m, k)), t).cpu().numpy().reshape(m, n)
         assert np.all(np.isfinite(y))
         assert_q4_close(y, x.reshape(m, k), w.astype(np.float32), what=f"f16 |w| >= 256, policy {policy}")
+
+
+# ------------------------------- encoder GEMM: LDS-DMA ring kernel (wq4_enc.hip) --
+@pytest.mark.parametrize("m,n,k,flags", [(1500, 1280, 1280, 0), (3000, 3840, 1280, 0), (700, 5120, 1280, 5),
+                                         (300, 1280, 5120, 2), (2049, 1280, 1280, 1), (16000, 1280, 1280, 2),
+                                         (4500, 5120, 1280, 5), (200, 96, 160, 0), (1000, 1312, 1280, 4)])
+def test_enc_kernel_bit_identical(torch, m, n, k, flags):
+    """The encoder-size GEMM ring kernel (its geometries: 256 x 256 with 8
+    waves, 64 x 128 and 32 x 256 with 4) gives the prefill tile kernel's bits
+    exactly: the same
+    per-block MFMA chain and scale FMA order, only the memory pipeline
+    differs.  flags: 1 GELU, 2 residual, 4 A-tiled output (then compared
+    fragment for fragment, padding included)."""
+    import ctypes
+
+    rng = np.random.default_rng(m + n + k + flags)
+    q = oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.05).astype(np.float32))
+    t = wq4.Q4Tensor.from_q4_bytes(q, [n, k])
+    L = wq4.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    p = lambda a: ctypes.c_void_p(a.data_ptr()) if a is not None else None  # noqa: E731
+    x = to_dev(torch, rng.standard_normal(m * k).astype(np.float32), (m, k))
+    at = torch.zeros(L.wq4_atiled_bytes(m, k, 0), dtype=torch.uint8, device="cuda:0")
+    wq4.check(L.wq4_tile_activations(p(x), m, k, k, 0, p(at), at.numel(), st))
+    b = to_dev(torch, (rng.standard_normal(n) * 0.1).astype(np.float32), (n,))
+    res = to_dev(torch, rng.standard_normal(m * n).astype(np.float32), (m, n))
+    tiled = (flags & 4) != 0
+    outs = []
+    prev = L.wq4_debug_set_enc_kernel(0)
+    try:
+        for mode in (0, 2, 3, 4, 1):
+            assert L.wq4_debug_set_enc_kernel(mode) >= 0
+            y = res.clone() if flags & 2 else torch.full((m, n), 7.0, device="cuda:0")
+            ot = torch.full((L.wq4_atiled_bytes(m, n, 0),), 0x5A, dtype=torch.uint8, device="cuda:0") if tiled else None
+            wq4.check(L.wq4_gemm_tiled(t.handle, p(b), p(at), p(y) if flags & 2 else None, None if tiled else p(y),
+                                       p(ot), m, flags, 0, 1, st))
+            torch.cuda.synchronize()
+            outs.append((ot if tiled else y).cpu().numpy().copy())
+    finally:
+        L.wq4_debug_set_enc_kernel(prev)
+    ref = outs[0]
+    for mode, o in zip((2, 3, 4, 1), outs[1:]):
+        if tiled:
+            assert np.array_equal(o, ref), f"A-tiled output differs in mode {mode}"
+        else:
+            assert np.array_equal(o.view(np.uint32), ref.view(np.uint32)), \
+                f"mode {mode}: {np.count_nonzero(o != ref)} of {o.size} outputs differ, max |d| {np.max(np.abs(o - ref))}"

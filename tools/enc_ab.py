@@ -1,0 +1,71 @@
+"""A/B timing of the encoder-size Q4 GEMM kernels in ONE process
+(cdna_hip_programming.md §5.4 rule 24): the prefill tile kernel (mode 0)
+against the LDS-DMA ring kernel's two geometries (2: 256 x 256, 3: 64 x 128),
+switched with wq4_debug_set_enc_kernel, on the four Large-V3 encoder shapes,
+interleaved over ROUNDS rounds on the same random operands.  Prints median /
+min ms and algorithmic TFLOP/s (2 M N K) per (shape, mode).
+
+    ROWS=48000 python tools/enc_ab.py      (env: ROWS, ROUNDS, REPS, MODES)
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "whisper-burn_amd"))
+sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
+
+import oracle  # noqa: E402
+import wq4  # noqa: E402
+
+M = int(os.environ.get("ROWS", "48000"))
+ROUNDS = int(os.environ.get("ROUNDS", "5"))
+REPS = int(os.environ.get("REPS", "5"))
+MODES = [int(v) for v in os.environ.get("MODES", "0,2,3").split(",")]
+SHAPES = [(3840, 1280), (1280, 1280), (5120, 1280), (1280, 5120)]
+
+
+def main():
+    L = wq4.lib()
+    vp = ctypes.c_void_p
+    st = vp(torch.cuda.current_stream().cuda_stream)
+    rng = np.random.default_rng(0)
+    setups = []
+    for n, k in SHAPES:
+        q = oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.05).astype(np.float32))
+        t = wq4.Q4Tensor.from_q4_bytes(q, [n, k], decode_step=False)
+        x = torch.randn(M, k, device="cuda")
+        at = torch.empty(L.wq4_atiled_bytes(M, k, 0), dtype=torch.uint8, device="cuda")
+        wq4.check(L.wq4_tile_activations(vp(x.data_ptr()), M, k, k, 0, vp(at.data_ptr()), at.numel(), st))
+        y = torch.empty(M, n, device="cuda")
+        setups.append((n, k, t, at, y))
+    torch.cuda.synchronize()
+    times = {}
+    prev = L.wq4_debug_set_enc_kernel(1)
+    for _ in range(ROUNDS):
+        for si, (n, k, t, at, y) in enumerate(setups):
+            for mode in MODES:
+                L.wq4_debug_set_enc_kernel(mode)
+                run = lambda: wq4.check(L.wq4_gemm_tiled(t.handle, None, vp(at.data_ptr()), None, vp(y.data_ptr()), None,
+                                                         M, 0, 0, 1, st))
+                run()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(REPS):
+                    run()
+                e.record()
+                torch.cuda.synchronize()
+                times.setdefault((si, mode), []).append(s.elapsed_time(e) / REPS)
+    L.wq4_debug_set_enc_kernel(prev)
+    for si, (n, k, *_rest) in enumerate(setups):
+        for mode in MODES:
+            a = np.array(times[(si, mode)])
+            print(f"N={n:5d} K={k:5d} M={M} mode {mode}: median {np.median(a):.4f} ms min {a.min():.4f} "
+                  f"-> {2 * M * n * k / np.median(a) / 1e9:7.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -57,6 +57,14 @@ hipError_t launch_q4_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* s
                           const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int ns, const DecodeWs* ws,
                           hipStream_t st, int wtype);
 
+// The encoder-size GEMM ring kernel (wq4_enc.hip): Q4_0 weights, f16x2
+// operands, f32 or A-tiled outputs, rows > 128 -- bit-identical to the
+// prefill tile kernel's results.  enc_gemm_pick: 0 = use the tile kernel,
+// else the geometry (2 = L, 3 = S) to pass to launch_enc_gemm.
+int enc_gemm_pick(const Q4Geom& g, int rows, int epi_mode, int ns, int wtype);
+hipError_t launch_enc_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* cs,
+                           const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int geo, hipStream_t st);
+
 // The decode-step GEMM (wq4_skinny.hip): rows <= 32, 16-column workgroups on
 // 16x16x32 MFMAs, one Q4 block per MFMA with the scale applied per block in
 // f32.  Its own weight layout (q16 / d16, or f16s for f16 weights) is built

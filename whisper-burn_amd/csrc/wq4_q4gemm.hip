@@ -38,6 +38,13 @@
 
 namespace wq4 {
 
+// WQ4_PF_DIAG (timing diagnostics of the prefill kernel only; 0 in the
+// product): 1 no scale FMAs, 2 no dequantisation, 3 scalar v_fma_f32 scale,
+// 4 = 1 + 2.
+#ifndef WQ4_PF_DIAG
+#define WQ4_PF_DIAG 0
+#endif
+
 // ------------------------------------------------------------------------
 // f32 row-major [M, K] -> A-tiled f16 (hi[, lo]) operand.  One thread per
 // (m-tile, block, kk, lane) = 8 elements.
@@ -257,6 +264,12 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
           // (mt, 1), so no FMA waits on the MFMA it reads
           static_assert(TN == 2, "the interleave below pairs the two n-tiles of a wave");
           floatx16 t0, t1;
+#if WQ4_PF_DIAG == 2 || WQ4_PF_DIAG == 4  // timing diagnostics: no dequantisation (raw bits as B)
+#pragma unroll
+          for (int nt = 0; nt < TN; ++nt)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) qf[nt][kk] = __builtin_bit_cast(half8, braw[nt][0]);
+#endif
           auto chain = [&](const half8 (&ah)[2], const half8 (&al)[2], int nt) {
             floatx16 t = mfma32(ah[0], qf[nt][0], floatx16{});
             if constexpr (NS == 2) t = mfma32(al[0], qf[nt][0], t);
@@ -273,10 +286,26 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
               ahi[kk] = *reinterpret_cast<const half8*>(fa + kk * NS * 1024);
               if constexpr (NS == 2) alo[kk] = *reinterpret_cast<const half8*>(fa + kk * NS * 1024 + 1024);
             }
+#if WQ4_PF_DIAG == 1 || WQ4_PF_DIAG == 4  // timing diagnostics: no scale FMAs (chains add into acc)
+            t0 = chain(ahi, alo, 0);
+            t1 = chain(ahi, alo, 1);
+            acc[mt][0] += t0;  // one v_add per element instead of an FMA would still be VALU: keep adds
+            acc[mt][1] += t1;
+#elif WQ4_PF_DIAG == 3  // scalar v_fma_f32 per element (build with -fno-slp-vectorize)
+            t0 = chain(ahi, alo, 0);
+            if (mt > 0) {
+#pragma unroll
+              for (int i = 0; i < 16; ++i) acc[mt - 1][1][i] = __builtin_fmaf(t1[i], dsc[1], acc[mt - 1][1][i]);
+            }
+            t1 = chain(ahi, alo, 1);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[mt][0][i] = __builtin_fmaf(t0[i], dsc[0], acc[mt][0][i]);
+#else
             t0 = chain(ahi, alo, 0);
             if (mt > 0) acc[mt - 1][1] = t1 * dsc[1] + acc[mt - 1][1];
             t1 = chain(ahi, alo, 1);
             acc[mt][0] = t0 * dsc[0] + acc[mt][0];
+#endif
             // issue order: the m-tile's 4 A reads, then MFMA / 2 VALU pairs
             __builtin_amdgcn_sched_group_barrier(0x100, 2 * NS, 0);
 #pragma unroll
@@ -285,7 +314,12 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
               __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
             }
           }
+#if WQ4_PF_DIAG == 3
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[TM - 1][1][i] = __builtin_fmaf(t1[i], dsc[1], acc[TM - 1][1][i]);
+#elif WQ4_PF_DIAG != 1 && WQ4_PF_DIAG != 4
           acc[TM - 1][1] = t1 * dsc[1] + acc[TM - 1][1];
+#endif
         }
       }
     }
@@ -1057,6 +1091,8 @@ static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint3
       }
     }
 #undef WQ4_DEC
+  } else if (const int geo = enc_gemm_pick(g, rows, EPI, NS, WK)) {
+    return launch_enc_gemm(g, nib, sc, cs, at, rows, e, EPI, geo, st);
   } else {
     const int ngroups = (int)((g.ntiles + 4 * kPrefillTN - 1) / (4 * kPrefillTN));
     const int mgroups = mtiles / kPrefillTM;

@@ -80,6 +80,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.wq4_tensor_create_ex.argtypes = [c_int, u8p, c_sz, c_i64, c_i64, ctypes.c_uint, ctypes.POINTER(vp)]
     L.wq4_tensor_create_f16_ex.argtypes = [c_int, ctypes.POINTER(ctypes.c_uint16), c_i64, c_i64, ctypes.c_uint,
                                            ctypes.POINTER(vp)]
+    L.wq4_debug_set_enc_kernel.argtypes = [c_int]
+    L.wq4_debug_set_enc_kernel.restype = c_int
     L.wq4_tensor_has_decode_step.argtypes = [vp]
     L.wq4_tensor_has_decode_step.restype = c_int
     L.wq4_tensor_weight_type.argtypes = [vp]
