@@ -1,6 +1,6 @@
 """Encoder-size Q4 GEMM probe: q4_matmul at M rows over the Large-V3 encoder
 shapes (N, K), REPS launches each, HIP-event timed; prints TFLOP/s per shape
-(algorithmic 2 M N K).  Used under rocprofv3 (scripts/gpu_gemm_prof.sh)."""
+(algorithmic 2 M N K).  Used under rocprofv3 (round 2; round 3: tools/enc_ab.py, scripts/gpu.sh gemm)."""
 import os
 import sys
 

@@ -1,0 +1,132 @@
+# One parameterised driver for every GPU-side measurement (run from the repo
+# root on the GPU box, e.g.  gpurun -- bash scripts/gpu.sh suite bench).
+# Tasks run in the order given; the first failure ends the call (no retries).
+# Results land in gpurun_out/$OUT (default gpurun_out/run); the ones the docs
+# cite are copied into profiles/ by hand.
+#
+#   suite           GPU parity suite (-m gpu, verbose prints) + smoke()
+#   bench           default bench line                        -> bench.json
+#   configs         BASELINE configs 2, 3, 5 (32 / 1 clip) and f16 precision
+#   trace           kernel trace of the bench's decode (BENCH_ARGS; 24 tokens):
+#                   tools/timeline.py, per-grid durations, in-graph xattn summary
+#   pmc             FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic.json
+#   stats           rocprofv3 --kernel-trace --stats of one bench step
+#   gemm            encoder GEMM kernels A/B (tools/enc_ab.py, ROWS list) + MFMA PMC
+#   groups          bench at WA_DECODE_GROUPS in $GLIST
+#   env             bench under each ';'-separated assignment list in $ENVLIST
+#   libs            bench with library variants whisper-burn_amd/diag/<v>/$LIB ($VARIANTS)
+#   round           suite, trace, pmc, stats, gemm, bench -- the round-end set
+#
+# Env: OUT (subdir), ROUND (tag), BENCH_ARGS (extra bench.py args).
+set -o pipefail
+O=gpurun_out/${OUT:-run}
+R=${ROUND:-r03}
+mkdir -p "$O"
+export TMPDIR=/tmp
+ROOT=$(pwd)
+
+bench_line() {  # name, bench args...
+  local n=$1; shift
+  timeout -k 10 600 python bench.py "$@" --json-out "$O/$n.json" > "$O/$n.log" 2>&1 || { tail -20 "$O/$n.log"; return 1; }
+  python3 -c "import json; d=json.load(open('$O/$n.json')); print('$n', d['value'], d['unit'], d['phase_ms'], 'xattn us', d['roofline_cross_attention']['avg_us'], 'q4 TF', d['roofline_q4_gemm']['achieved'])"
+}
+
+trace_csv() {  # dir -> the kernel_trace.csv rocprofv3 wrote under it
+  ls "$1"/*/run_kernel_trace.csv "$1"/run_kernel_trace.csv 2>/dev/null | head -1
+}
+
+task_suite() {
+  timeout -k 10 900 python -u -m pytest tests -q -m gpu -s --timeout 300 --timeout-method thread -rf > "$O/pytest_gpu.log" 2>&1
+  local rc=$?
+  grep -E "passed|failed|worst|tokens equal|FAILED" "$O/pytest_gpu.log" | tail -30
+  [ $rc -eq 0 ] || return $rc
+  timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || return 1
+  tail -1 "$O/smoke.log"
+}
+
+task_bench() { bench_line bench $BENCH_ARGS; }
+
+task_configs() {
+  bench_line c2_medium_b1 --variant medium --clips-per-gpu 1 --no-cpu-baseline || return 1
+  bench_line c3_large_v3_b1 --clips-per-gpu 1 --no-cpu-baseline || return 1
+  bench_line c5_large_v3_f16w --weights f16 || return 1
+  bench_line c5_large_v3_f16w_b1 --weights f16 --clips-per-gpu 1 --no-cpu-baseline || return 1
+  bench_line c4_precision_f16 --precision f16 --no-cpu-baseline
+}
+
+task_trace() {
+  timeout -k 10 600 rocprofv3 --kernel-trace -d "$O/trace" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 \
+    --max-tokens 24 --fixed-length --no-cpu-baseline $BENCH_ARGS > "$O/trace.log" 2>&1 || { tail "$O/trace.log"; return 1; }
+  local f; f=$(trace_csv "$O/trace")
+  python3 tools/timeline.py "$f" > "$O/timeline.txt" || return 1
+  python3 scripts/trace_by_grid.py "$f" "skinny|q4_gemm_decode|xattn|dec_self|logits" "$O/chain_grid.json" > /dev/null || return 1
+  python3 scripts/in_graph_summary.py "$O/chain_grid.json" large_v3 q4_0 f16x2 32 "$O/xattn_in_graph.json" || return 1
+  cat "$O/timeline.txt"
+  gzip -f "$f"
+}
+
+task_pmc() {
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "q4_gemm|xattn" -d "gpurun_out/pmc_${C}_$R" -o run --output-format csv \
+      -- python3 bench.py --steps 1 --warmup 0 --max-tokens 8 --no-cpu-baseline $BENCH_ARGS > "$O/pmc_$C.log" 2>&1 || return 1
+  done
+  python3 scripts/pmc_summary.py $R "$O/pmc_traffic.json" > "$O/pmc_summary.log" || return 1
+  rm -f gpurun_out/pmc_*_$R/*/run_counter_collection.csv gpurun_out/pmc_*_$R/run_counter_collection.csv
+  tail -5 "$O/pmc_summary.log"
+}
+
+task_stats() {
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/stats" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 \
+    --no-cpu-baseline $BENCH_ARGS --json-out "$O/bench_under_rocprof.json" > "$O/stats.log" 2>&1 || return 1
+  cp "$(ls "$O"/stats/*/run_kernel_stats.csv "$O"/stats/run_kernel_stats.csv 2>/dev/null | head -1)" "$O/kernel_stats.csv"
+  rm -f "$(trace_csv "$O/stats")"
+  python3 scripts/kstats.py "$O/kernel_stats.csv" 20
+}
+
+task_gemm() {
+  for r in ${ROWS_LIST:-1500 48000}; do
+    ROWS=$r MODES=${MODES:-0,3} timeout -k 10 300 python -u tools/enc_ab.py > "$O/enc_ab_$r.log" 2>&1 || return 1
+    grep -v amdgpu.ids "$O/enc_ab_$r.log"
+  done
+  cd /tmp
+  ROWS=48000 MODES=0 ROUNDS=1 REPS=2 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
+    SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-include-regex "prefill|q4_gemm_enc" \
+    -d "$ROOT/$O/gemm_pmc" -o run --output-format csv -- python3 "$ROOT/tools/enc_ab.py" > "$ROOT/$O/gemm_pmc.log" 2>&1 || { cd "$ROOT"; return 1; }
+  cd "$ROOT"
+  python3 scripts/mfma_summary.py "$O/gemm_pmc" | tee "$O/q4_gemm_mfma.txt"
+}
+
+task_groups() {
+  for G in ${GLIST:-1 2 3}; do
+    WA_DECODE_GROUPS=$G bench_line groups_$G --no-cpu-baseline $BENCH_ARGS || return 1
+  done
+}
+
+task_env() {
+  local i=0
+  IFS=';' read -ra RUNS <<< "$ENVLIST"
+  for E in "${RUNS[@]}"; do
+    i=$((i + 1))
+    echo "env $i: $E"
+    ( export $E; bench_line env_$i --no-cpu-baseline $BENCH_ARGS ) || return 1
+  done
+}
+
+task_libs() {
+  local L=${LIB:-libwq4.so}
+  cp whisper-burn_amd/lib/$L /tmp/$L.base
+  for V in base ${VARIANTS} base; do
+    if [ "$V" = base ]; then cp /tmp/$L.base whisper-burn_amd/lib/$L; else cp whisper-burn_amd/diag/$V/$L whisper-burn_amd/lib/$L; fi
+    bench_line lib_$V --no-cpu-baseline $BENCH_ARGS || { cp /tmp/$L.base whisper-burn_amd/lib/$L; return 1; }
+  done
+}
+
+task_round() {
+  task_suite && task_trace && task_pmc && task_stats && task_gemm && task_bench
+}
+
+[ $# -gt 0 ] || { sed -n 2,24p "$0"; exit 2; }
+for t in "$@"; do
+  echo "== $t"
+  "task_$t" || { echo "task $t failed"; exit 1; }
+done

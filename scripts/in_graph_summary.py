@@ -7,5 +7,5 @@ import sys
 grid, variant, weights, prec, clips, out = sys.argv[1:7]
 rows = [e for e in json.load(open(grid)) if e["kernel"].startswith("xattn")]
 json.dump({"workload": {"variant": variant, "weights": weights, "precision": prec, "clips": int(clips)},
-           "source": "rocprofv3 --kernel-trace of bench.py (scripts/gpu_chain_trace.sh), decode graphs replayed",
+           "source": "rocprofv3 --kernel-trace of bench.py (scripts/gpu.sh trace), decode graphs replayed",
            "kernels": rows}, open(out, "w"), indent=1)

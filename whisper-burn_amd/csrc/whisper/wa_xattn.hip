@@ -55,7 +55,7 @@ constexpr float kWkScale = 4096.0f, kXqInv = 1.0f / (16.0f * 4096.0f);
 constexpr float kQtScale = 32.0f, kEncScale = 32.0f, kSInv = 1.0f / 1024.0f;
 constexpr float kPScale = 16384.0f, kZInv = 1.0f / (16384.0f * 32.0f);
 constexpr float kZnScale = 32.0f, kWvScale = 4096.0f, kOutInv = 1.0f / (32.0f * 4096.0f);
-#ifndef WA_XATTN_SPLITS  // compile-time only: tuning builds of scripts/gpu_xattn_splits.sh
+#ifndef WA_XATTN_SPLITS  // compile-time only: tuning builds (A/B: scripts/gpu.sh libs)
 #define WA_XATTN_SPLITS 8
 #endif
 // Frame ranges per query row.  Measured: 8 beat 4, 6, 12 and 16 in round 1;
@@ -995,7 +995,7 @@ void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T,
 // Rows of Zn per xattn_out workgroup: 4.  Isolated, 2 rows per workgroup is
 // faster at 16 rows (9.6 vs 11.0 us) and slower at 32 (14.3 vs 11.1); in the
 // model (two concurrent 16-row decode groups) 2 rows made the decode slower
-// (893-898 vs 874-878 ms, scripts/gpu_ab_outrows.sh): the doubled grid
+// (893-898 vs 874-878 ms, scripts/gpu.sh libs): the doubled grid
 // crowds the other group.  1 and 8 are slower everywhere.  A row's bits do
 // not depend on its workgroup's rows (each is its own MFMA column).
 #ifndef WA_XATTN_OUT_ROWS  // compile-time override: tuning builds (scripts/xattn_micro.sh)

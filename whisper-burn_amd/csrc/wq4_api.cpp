@@ -185,7 +185,7 @@ int pick_kernel(const wq4_tensor* w, int64_t rows, int kernel) {
 // -- in the model's decode step, two groups' chains run concurrently and its
 // 40-160 workgroup grids left room for the other group's kernels: decode
 // 875 ms against 905-914 ms with the decode-step kernel's 80-240 workgroups
-// (Large-V3, 32 clips, scripts/gpu_ab_lnfold.sh, r02) -- else the decode-step
+// (Large-V3, 32 clips, bench A/B, r02) -- else the decode-step
 // kernel (3), which policy 3 also forces; 0 = unsupported.
 int lnfold_kernel(const wq4_tensor* w, int64_t rows) {
   if (!w || w->flat || rows < 1 || rows > 32) return 0;

@@ -539,7 +539,7 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
 
   // this wave's weights (once-read stream: nt) -- zeros past cnt
   const size_t t0 = (size_t)nt * nbp + bp0;
-  // WQ4_DIAG (timing diagnostics only, scripts/gpu_diag.sh; 0 in the product):
+  // WQ4_DIAG (timing diagnostics only, make diag + scripts/gpu.sh libs; 0 in the product):
   // 1 no MFMAs, 2 no A loads, 3 no weight loads, 4 no epilogue
   constexpr int kDiag = WQ4_DIAG;
   constexpr int BW = WK == kWeightsF16 ? 4 : 1;  // 16 B weight loads per lane per bp

@@ -16,7 +16,7 @@
 //
 // Why 16 columns: a K = 1280 decode GEMM at 32 columns per workgroup runs on
 // 40 of 256 CUs and its dependent MFMA chain alone took 2.4 us of a 7.2 us
-// kernel (scripts/gpu_diag.sh, WQ4_DIAG = 1); 16 columns double the CUs and
+// kernel (WQ4_DIAG = 1 timing build); 16 columns double the CUs and
 // the 16x16x32 shape does not pad 16 rows to 32.
 //
 // Weight layout (built once at upload, beside the prefill kernel's):

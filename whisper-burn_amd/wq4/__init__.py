@@ -20,7 +20,7 @@ import numpy as np
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # WQ4_LIB_DIR: load the libraries from another build directory (the timing
-# diagnostics of scripts/gpu_diag.sh); the product build is lib/.
+# diagnostics: `scripts/gpu.sh libs` / WQ4_LIB_DIR); the product build is lib/.
 LIB_PATH = os.path.join(os.environ.get("WQ4_LIB_DIR") or os.path.join(_PKG_ROOT, "lib"), "libwq4.so")
 HEADER_PATH = os.path.join(os.path.dirname(_PKG_ROOT), "include", "wq4.h")
 
