@@ -19,7 +19,7 @@ for r in rows:
     m = re.search(r"[a-z][a-z0-9]*(?:_[a-z0-9]+)*_kernel", r["Kernel_Name"])
     name = m.group(0) if m else r["Kernel_Name"][:40]
     if "q4_gemm_decode" in name or "skinny" in name:
-        name = f"{name}[{r['Grid_Size']}]"
+        name = f"{name}[{r.get('Grid_Size_X', r.get('Grid_Size', ''))}]"
     K.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Queue_Id", "0"), name))
 K.sort()
 dec = re.compile(r"xattn|dec_self|q4_gemm_decode|skinny_gemm|logits_argmax|embed_fold|bookkeep")
@@ -57,20 +57,30 @@ for n, (a, b) in sorted(fam.items(), key=lambda kv: -sum(kv[1][0]) - sum(kv[1][1
     allv = a + b
     f = lambda v: f"{sum(v) / len(v):8.2f}" if v else "       -"
     print(f"{n[:48]:48s} {len(allv):6d} {sum(allv) / len(allv):8.2f} {f(a)} {len(a):6d} {f(b):>11s} {len(b):6d}")
-# concurrency histogram over the decode window
-ev = []
-for s, e, q, n in D:
-    ev.append((s, 1))
-    ev.append((e, -1))
-ev.sort()
-cnt, last = 0, ev[0][0]
-hist = collections.Counter()
-for t, d in ev:
-    hist[min(cnt, 3)] += t - last
-    cnt += d
-    last = t
-tot = sum(hist.values())
-print("in flight: " + ", ".join(f"{k if k < 3 else '3+'}: {v / tot:.1%}" for k, v in sorted(hist.items())))
+# decode phases: runs of decode kernels separated by > 1 ms with none in flight
+runs, cur = [], [D[0]]
+for k in D[1:]:
+    if k[0] - max(x[1] for x in cur[-64:]) > 1_000_000:
+        runs.append(cur)
+        cur = []
+    cur.append(k)
+runs.append(cur)
+for i, run in enumerate(runs):
+    ev = []
+    for s, e, q, n in run:
+        ev.append((s, 1))
+        ev.append((e, -1))
+    ev.sort()
+    cnt, last = 0, ev[0][0]
+    hist = collections.Counter()
+    for t, d in ev:
+        hist[min(cnt, 3)] += t - last
+        cnt += d
+        last = t
+    tot = sum(hist.values())
+    steps = sum(1 for k in run if k[3] == "wa28logits_argmax_f16_k32_kernel") / max(1, len(queues))
+    print(f"decode run {i}: {tot * 1e-6:.2f} ms, {len(run)} kernels, ~{steps:.0f} steps per group; kernels in flight: "
+          + ", ".join(f"{k if k < 3 else '3+'}: {v / tot:.1%}" for k, v in sorted(hist.items())))
 # main-vs-main overlap
 ov = 0
 for q in queues:
