@@ -67,6 +67,37 @@ __device__ __forceinline__ void atile_store4(_Float16* t, int row, int k, int kb
   if constexpr (NS == 2) *reinterpret_cast<half4*>(t + atile_index(row, k, kbp, NS, 1)) = lo;
 }
 
+// LayerNorm-fold consumer: a row's mean and sqrt(var + eps) from its
+// `tiles` 16-column tile statistics (tile mean m_j, sum of squared
+// deviations q_j), spread over 16 consecutive lanes (part p holds tiles p,
+// p + 16, ...; zeros past `tiles`).  Every tile holds 16 values, so the
+// exact merge is the equal-count one:
+//   mean = (sum_j m_j) / T,   M2 = sum_j q_j + 16 sum_j (m_j - mean)^2
+// -- two passes, two divisions per row (the per-step divisions of a
+// pairwise merge cost ~1.7 us per launch on the decode critical path,
+// tools/warm_cold.py).  The cross-lane sums are xor butterflies; a + b is
+// commutative bit-for-bit, so every lane and every workgroup gets the same
+// bits, and the result depends on (K, the statistics) only.
+template <int NPER>
+__device__ __forceinline__ void lnf_merge_tiles(const floatx2 (&st)[NPER], int part, int tiles, float& mean,
+                                                float& den) {
+  float s = 0.0f;
+#pragma unroll
+  for (int v = 0; v < NPER; ++v) s += part + 16 * v < tiles ? st[v][0] : 0.0f;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+  mean = s / (float)tiles;
+  float q = 0.0f;
+#pragma unroll
+  for (int v = 0; v < NPER; ++v) {
+    const float d = st[v][0] - mean;
+    q += part + 16 * v < tiles ? st[v][1] + 16.0f * (d * d) : 0.0f;
+  }
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o, 64);
+  den = sqrtf(q / (float)(16 * tiles) + 1e-5f);
+}
+
 __host__ __device__ inline int kbp_of(int k) { return ((k / 32 + 1) / 2) * 2; }
 
 __device__ __forceinline__ float ln_apply(float v, float mean, float den, float g, float b) {

@@ -505,17 +505,27 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
   // acc_row(2 wave + q, h), column nt * 32 + r) are loaded up front so they
   // are not a memory round trip after the MFMAs (bias, residual: never
   // written by this launch before its own epilogue reads them).
+  // All of these are branch-free buffer loads (an absent operand is a
+  // zero-size resource, an out-of-range element an out-of-range offset: both
+  // read 0): a load under an exec branch made the compiler drain vmcnt(0)
+  // at the join, one full memory latency before the weight stream was even
+  // issued (+1.9 us per LayerNorm-fold consumer launch, tools/warm_cold.py).
   float pre_bias = 0.0f, pre_res[2] = {0.0f, 0.0f};
   float pre_wg = 0.0f, pre_g = 0.0f;  // LayerNorm fold: W gamma[col] (consumer), gamma[col] (producer)
   if constexpr (W == 8 && EPI != kEpiHeadMajor) {
     const int col = nt * 32 + r;
-    if (e.bias && col < e.n) pre_bias = e.bias[col];
-    if (e.lnf_stats_in && col < e.n) pre_wg = e.lnf_wg[col];
-    if (e.lnf_at && col < e.n) pre_g = e.lnf_g[col];
+    const int coff = col < e.n ? col * 4 : kOob;
+    const uint32_t nb = (uint32_t)e.n * 4;
+    pre_bias = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brsrc(e.bias, e.bias ? nb : 0), coff, 0, 0));
+    pre_wg = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                           brsrc(e.lnf_wg, e.lnf_stats_in ? nb : 0), coff, 0, 0));
+    pre_g = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brsrc(e.lnf_g, e.lnf_at ? nb : 0), coff, 0, 0));
+    const __amdgpu_buffer_rsrc_t rres = brsrc(e.residual, e.residual ? (uint32_t)e.m * (uint32_t)e.ldo * 4 : 0);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int row = mt0 * 32 + acc_row(2 * wave + q, lane >> 5);
-      if (e.residual && row < e.m && col < e.n) pre_res[q] = e.residual[(size_t)row * e.ldo + col];
+      pre_res[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 rres, row < e.m && col < e.n ? (row * e.ldo + col) * 4 : kOob, 0, 0));
     }
   }
   // LayerNorm fold, consumer: thread (row tid / 16, part tid % 16) loads the
@@ -525,17 +535,21 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
   floatx2 lnf_st[kLnfPer];
   const int lnf_row = tid >> 4, lnf_part = tid & 15;
   if constexpr (W == 8) {
-    if (e.lnf_stats_in) {
-      const int grow = mt0 * 32 + lnf_row;
+    const int grow = mt0 * 32 + lnf_row;
+    const __amdgpu_buffer_rsrc_t rst =
+        brsrc(e.lnf_stats_in, e.lnf_stats_in ? (uint32_t)e.m * (uint32_t)e.lnf_tiles * 8 : 0);
 #pragma unroll
-      for (int u = 0; u < kLnfPer; ++u) {
-        const int j = lnf_part + 16 * u;
-        lnf_st[u] = (grow < e.m && j < e.lnf_tiles)
-                        ? *reinterpret_cast<const floatx2*>(e.lnf_stats_in + ((size_t)grow * e.lnf_tiles + j) * 2)
-                        : floatx2{0.0f, 0.0f};
-      }
+    for (int u = 0; u < kLnfPer; ++u) {
+      const int j = lnf_part + 16 * u;
+      lnf_st[u] = __builtin_bit_cast(floatx2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                  rst, grow < e.m && j < e.lnf_tiles ? (grow * e.lnf_tiles + j) * 8 : kOob, 0, 0));
     }
   }
+  // keep every epilogue-operand / statistics load above the weight stream
+  // (the merge below then waits for them with a counted vmcnt)
+#ifndef WQ4_NO_SB
+  __builtin_amdgcn_sched_barrier(0);
+#endif
 
   // this wave's weights (once-read stream: nt) -- zeros past cnt
   const size_t t0 = (size_t)nt * nbp + bp0;
@@ -655,42 +669,18 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
     }
   }
 
-  // LayerNorm fold, consumer: Chan et al. merge of the row's tile
-  // statistics (every tile 32 columns), then over the 16 parts of the row by
-  // a butterfly in which the lower lane is always the left operand, so every
-  // lane -- and every workgroup of the launch -- gets the same bits.
+  // LayerNorm fold, consumer: the row statistics from its tile statistics
+  // (lnf_merge_tiles, wq4_lnmath.hpp)
   float* lnf_mu = reinterpret_cast<float*>(smem + decode_lds_bytes_dev(W) + 2 * 64 * 4);  // [32]
   float* lnf_den = lnf_mu + 32;                                                           // [32]
   float* lnf_x = lnf_den + 32;                                                            // [32][33]
   if constexpr (W == 8) {
     if (e.lnf_stats_in) {
-      float n_a = 0.0f, m_a = 0.0f, q_a = 0.0f;
-#pragma unroll
-      for (int u = 0; u < kLnfPer; ++u) {
-        if (lnf_part + 16 * u < e.lnf_tiles) {
-          const float n = n_a + 16.0f, d = lnf_st[u][0] - m_a;
-          m_a = m_a + d * (16.0f / n);
-          q_a = q_a + lnf_st[u][1] + d * d * (n_a * 16.0f / n);
-          n_a = n;
-        }
-      }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        const float n_b = __shfl_xor(n_a, o, 64), m_b = __shfl_xor(m_a, o, 64), q_b = __shfl_xor(q_a, o, 64);
-        const bool low = (lnf_part & o) == 0;
-        const float nl = low ? n_a : n_b, ml = low ? m_a : m_b, ql = low ? q_a : q_b;
-        const float nh = low ? n_b : n_a, mh = low ? m_b : m_a, qh = low ? q_b : q_a;
-        const float n = nl + nh;
-        if (n > 0.0f) {
-          const float d = mh - ml;
-          m_a = ml + d * (nh / n);
-          q_a = ql + qh + d * d * (nl * nh / n);
-        }
-        n_a = n;
-      }
+      float m_a, den_a;
+      lnf_merge_tiles<kLnfPer>(lnf_st, lnf_part, e.lnf_tiles, m_a, den_a);
       if (lnf_part == 0) {
         lnf_mu[lnf_row] = m_a;
-        lnf_den[lnf_row] = sqrtf(q_a / (float)(16 * e.lnf_tiles) + 1e-5f);
+        lnf_den[lnf_row] = den_a;
       }
     }
   }

@@ -275,37 +275,14 @@ __global__ __launch_bounds__(64 * kSkW) void skinny_gemm_kernel(const uint32_t* 
     if (bw0 + i < bw1) sk_compute<NT, MT, NS, WK>(Bk[i], acc);
   if constexpr (WQ4_STAMP) st_[2] = stamp_rt();
 
-  // LayerNorm fold, consumer: Chan et al. merge of the row's 16-column tile
-  // statistics, then a butterfly over the 16 parts in which the lower lane is
-  // always the left operand (every workgroup gets the same bits)
+  // LayerNorm fold, consumer: the row statistics from its 16-column tile
+  // statistics (lnf_merge_tiles, wq4_lnmath.hpp)
   if (e.lnf_stats_in) {
-    float n_a = 0.0f, m_a = 0.0f, q_a = 0.0f;
-#pragma unroll
-    for (int v = 0; v < kSkLnPer; ++v) {
-      if (lpart + 16 * v < e.lnf_tiles) {
-        const float nn = n_a + 16.0f, dd = lnf_st[v][0] - m_a;
-        m_a = m_a + dd * (16.0f / nn);
-        q_a = q_a + lnf_st[v][1] + dd * dd * (n_a * 16.0f / nn);
-        n_a = nn;
-      }
-    }
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      const float n_b = __shfl_xor(n_a, o, 64), m_b = __shfl_xor(m_a, o, 64), q_b = __shfl_xor(q_a, o, 64);
-      const bool low = (lpart & o) == 0;
-      const float nl = low ? n_a : n_b, ml = low ? m_a : m_b, ql = low ? q_a : q_b;
-      const float nh = low ? n_b : n_a, mh = low ? m_b : m_a, qh = low ? q_b : q_a;
-      const float nn = nl + nh;
-      if (nn > 0.0f) {
-        const float dd = mh - ml;
-        m_a = ml + dd * (nh / nn);
-        q_a = ql + qh + dd * dd * (nl * nh / nn);
-      }
-      n_a = nn;
-    }
+    float m_a, den_a;
+    lnf_merge_tiles<kSkLnPer>(lnf_st, lpart, e.lnf_tiles, m_a, den_a);
     if (lpart == 0 && tid < 256) {
       lnf_mu[lrow - r0] = m_a;
-      lnf_den[lrow - r0] = sqrtf(q_a / (float)(16 * e.lnf_tiles) + 1e-5f);
+      lnf_den[lrow - r0] = den_a;
     }
   }
 
