@@ -547,9 +547,7 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
   }
   // keep every epilogue-operand / statistics load above the weight stream
   // (the merge below then waits for them with a counted vmcnt)
-#ifndef WQ4_NO_SB
   __builtin_amdgcn_sched_barrier(0);
-#endif
 
   // this wave's weights (once-read stream: nt) -- zeros past cnt
   const size_t t0 = (size_t)nt * nbp + bp0;
