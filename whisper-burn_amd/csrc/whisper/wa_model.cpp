@@ -792,16 +792,6 @@ bool lnfold_on(const wa_model* m, int Tq, const wa::DecodeState* state, int64_t 
   return true;
 }
 
-// TEMPORARY removal ablation (timing only, wrong results): WA_SKIP bits
-// 1 qkv, 2 self, 4 out, 8 cq, 16 xattn, 32 cout, 64 fc1, 128 fc2
-int skip_bits() {
-  static const int v = [] {
-    const char* e = getenv("WA_SKIP");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 // A greedy decode step of <= 32 clips picks its tokens inside the logits
 // kernel (wa::launch_logits_argmax); prompts and larger groups keep the
 // stored logits + separate argmax.
@@ -835,45 +825,37 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
     DecLayer& L = m->dec[li];
     if (fold) {
       const wq4_ln_fold cons1{nullptr, nullptr, nullptr, g.ln_stats, L.qkv_wg};
-      if (!(skip_bits() & 1) || !state)
       WA_WQ4(wq4_gemm_tiled_lnfold(L.qkv, L.qkv_b2, g.atd_ln, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, &cons1,
                                    st));
     } else {
       WA_WQ4(wq4_layernorm(g.xd, L.ln1_w, L.ln1_b, rows, D, m->prec, g.atd_dec, nullptr, st));
       WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, g.atd_dec, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, 2, st));
     }
-    if (!(skip_bits() & 2) || !state)
     WA_HIP(wa::launch_decoder_self_attention(g.qkvd, L.cache_k + self_ofs, L.cache_v + self_ofs, B, Tq, H,
                                              c.n_text_ctx, state, kv0, g.atd_dec, m->ns, st));
     if (fold) {
       const wq4_ln_fold prod2{L.ln2_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
-      if (!(skip_bits() & 4) || !state)
       WA_WQ4(wq4_gemm_tiled_lnfold(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec,
                                    &prod2, st));
       const wq4_ln_fold cons2{nullptr, nullptr, nullptr, g.ln_stats, L.cq_wg};
-      if (!(skip_bits() & 8) || !state)
       WA_WQ4(wq4_gemm_tiled_lnfold(L.cq, L.cq_b2, g.atd_ln, nullptr, g.qd, nullptr, rows, 0u, m->prec, &cons2, st));
     } else {
       WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
       WA_WQ4(wq4_layernorm(g.xd, L.ln2_w, L.ln2_b, rows, D, m->prec, g.atd_dec, nullptr, st));
       WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, g.atd_dec, nullptr, g.qd, nullptr, rows, 0u, m->prec, 2, st));
     }
-    if (!(skip_bits() & 16) || !state)
     WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, Tq, T, H, D, g.xqt, g.xattn_part,
                             g.atd_dec, m->ns, st));
     if (fold) {
       const wq4_ln_fold prod3{L.ln3_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
-      if (!(skip_bits() & 32) || !state)
       WA_WQ4(wq4_gemm_tiled_lnfold(L.cout, L.cout_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL,
                                    m->prec, &prod3, st));
       const wq4_ln_fold cons3{nullptr, nullptr, nullptr, g.ln_stats, L.fc1_wg};
-      if (!(skip_bits() & 64) || !state)
       WA_WQ4(wq4_gemm_tiled_lnfold(L.fc1, L.fc1_b2, g.atd_ln, nullptr, nullptr, g.atf_dec, rows,
                                    WQ4_EPI_GELU | WQ4_EPI_TILED_OUT, m->prec, &cons3, st));
       // the next layer's attn_ln (none after the last layer: decoder.ln below)
       const wq4_ln_fold prod1{li + 1 < nl ? m->dec[li + 1].ln1_w : nullptr, li + 1 < nl ? g.atd_ln : nullptr,
                               li + 1 < nl ? g.ln_stats : nullptr, nullptr, nullptr};
-      if (!(skip_bits() & 128) || !state)
       WA_WQ4(wq4_gemm_tiled_lnfold(L.fc2, L.fc2_b, g.atf_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec,
                                    &prod1, st));
     } else {

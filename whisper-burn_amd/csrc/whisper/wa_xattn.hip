@@ -73,12 +73,6 @@ constexpr int kXattnSplits = WA_XATTN_SPLITS;
 #ifndef WA_XATTN_DIAG
 #define WA_XATTN_DIAG 0
 #endif
-#ifndef WA_XATTN_NW4  // A/B builds: 4-wave main workgroups at every D
-#define WA_XATTN_NW4 0
-#endif
-#ifndef WA_XATTN_PIPE  // main kernel loop order (A/B builds): 1 = software-pipelined staging
-#define WA_XATTN_PIPE 0
-#endif
 // xattn_out attribution builds (tools/xattn_micro.hip only, wrong results):
 // 1 = no Wv stage, 2 = no split-partial loads, 3 = no projection MFMAs.
 #ifndef WA_XATTN_ODIAG
@@ -385,8 +379,8 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
 #pragma unroll
     for (int ht = 0; ht < HT; ++ht) *reinterpret_cast<floatx4*>(&red[w][ht][l16][4 * lq]) = sacc[ht];
   };
-  // online softmax of the sub-chunk's scores (red) into sp / salpha / srescale
-  auto softmax_phase = [&](int chi, int t0) {
+  // online softmax of the sub-chunk's scores (red) and the Z update from se
+  auto tail = [&](int chi, int t0) {
     // online softmax: entry (head tile, head, frame); 16 lanes per head
 #pragma unroll
     for (int e = 0; e < SMX; ++e) {
@@ -409,27 +403,13 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
         if (alpha != 1.0f && WA_XATTN_DIAG != 5) srescale[chi & 1] = 1;  // benign race: every writer stores 1
       }
     }
-  };
-  // the Z update's B operands (enc, k = frame, n = column) of this wave's
-  // column tiles, read transposed from its own se slice
-  auto z_operands = [&](half8 (&ebr)[KS][NS]) {
-#pragma unroll
-    for (int ct = 0; ct < KS; ++ct)
-#pragma unroll
-      for (int p = 0; p < NS; ++p) {
-        const _Float16* base = &se[trow * RS + p * D + c0 + ct * 32 + tcol_sw];
-        const half4 x0 = lds_tr4(base);
-        const half4 x1 = lds_tr4(base + 4 * RS);
-        ebr[ct][p] = half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-      }
-  };
-  // after the softmax barrier: rescale, then Z += P enc (A = P, m = head, k = frame)
-  auto z_phase = [&](int chi, auto&& ebfrag) {
     if (WA_XATTN_DIAG != 7) __syncthreads();
     // alpha == 1 for every head (no running maximum moved, the steady state)
     // makes the rescale a multiplication by 1: skipped, bit-identical
     const bool rescale = srescale[chi & 1] != 0;
     if (tid == 0) srescale[(chi + 1) & 1] = 0;  // next sub-chunk's flag; its writers come after the next score barrier
+
+    // Z update: A = P (m = head, k = frame), B = enc (k = frame, n = column)
     half8 pa[NS];
 #pragma unroll
     for (int p = 0; p < NS; ++p) pa[p] = *reinterpret_cast<const half8*>(&sp[p][l32][8 * lh]);
@@ -445,74 +425,43 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     for (int ct = 0; ct < (WA_XATTN_DIAG == 2 ? 0 : KS); ++ct) {
       half8 eb[NS];
 #pragma unroll
-      for (int p = 0; p < NS; ++p) eb[p] = ebfrag(ct, p);
+      for (int p = 0; p < NS; ++p) {
+        const _Float16* base = &se[trow * RS + p * D + c0 + ct * 32 + tcol_sw];
+        const half4 x0 = lds_tr4(base);
+        const half4 x1 = lds_tr4(base + 4 * RS);
+        eb[p] = half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+      }
       zacc[ct] = mfma32x16(pa[0], eb[0], zacc[ct]);
-      if constexpr (NS == 2) {
+      if (NS == 2) {
         zacc[ct] = mfma32x16(pa[1], eb[0], zacc[ct]);
         zacc[ct] = mfma32x16(pa[0], eb[1], zacc[ct]);
       }
     }
   };
-  auto score_frag = [&](int ks, int p) {
-    return *reinterpret_cast<const half8*>(&se[l16 * RS + p * D + c0 + ks * 32 + 8 * lq_sw]);
+  // One sub-chunk: this wave's slice to se, the next fetch, the scores from
+  // se, then one barrier for the score partials and one inside tail().
+  auto step = [&](u32x4v (&buf)[NLD], int chi) {
+    const int t0 = ts + chi * kTc;
+    write_se(buf);
+    if (chi + PF < nch && WA_XATTN_DIAG != 1) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
+    scores([&](int ks, int p) {
+      return *reinterpret_cast<const half8*>(&se[l16 * RS + p * D + c0 + ks * 32 + 8 * lq_sw]);
+    });
+    if (WA_XATTN_DIAG != 6) __syncthreads();  // every wave's score partials in red
+    tail(chi, t0);
   };
-  if constexpr (WA_XATTN_PIPE) {
-    // Software-pipelined order (every se slice is private to its wave): the
-    // wave takes its Z operands of sub-chunk c into registers right after
-    // its scores, then overwrites its slice with sub-chunk c + 1 and issues
-    // the fetch of c + 2 -- all before the score barrier, so the staging
-    // write overlaps the other waves' scores and the softmax instead of
-    // opening the next sub-chunk.  Same arithmetic, same bits.
-    u32x4v buf[NLD];
-    if (nch > 0) fetch(buf, 0);
-    __syncthreads();  // sq1, sp, salpha, srescale, szero initialised
-    if (nch > 0) {
-      write_se(buf);
-      if (nch > 1) fetch(buf, 1);
-    }
-    for (int chi = 0; chi < nch; ++chi) {
-      const int t0 = ts + chi * kTc;
-      scores(score_frag);
-      half8 ebr[KS][NS];
-      z_operands(ebr);
-      if (chi + 1 < nch) {
-        write_se(buf);
-        if (chi + 2 < nch) fetch(buf, chi + 2);
-      }
-      __syncthreads();  // every wave's score partials in red
-      softmax_phase(chi, t0);
-      z_phase(chi, [&](int ct, int p) { return ebr[ct][p]; });
+  u32x4v pre0[NLD];
+  u32x4v pre1[PF == 2 ? NLD : 1];
+  if (nch > 0) fetch(pre0, 0);
+  __syncthreads();  // sq1, sp, salpha, srescale, szero initialised
+  if constexpr (PF == 2) {
+    if (nch > 1) fetch(pre1, 1);
+    for (int chi = 0; chi < nch; chi += 2) {
+      step(pre0, chi);
+      if (chi + 1 < nch) step(pre1, chi + 1);
     }
   } else {
-    // One sub-chunk: this wave's slice to se, the next fetch, the scores from
-    // se, then one barrier for the score partials and one before the Z update.
-    auto step = [&](u32x4v (&buf)[NLD], int chi) {
-      const int t0 = ts + chi * kTc;
-      write_se(buf);
-      if (chi + PF < nch && WA_XATTN_DIAG != 1) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
-      scores(score_frag);
-      if (WA_XATTN_DIAG != 6) __syncthreads();  // every wave's score partials in red
-      softmax_phase(chi, t0);
-      z_phase(chi, [&](int ct, int p) {
-        const _Float16* base = &se[trow * RS + p * D + c0 + ct * 32 + tcol_sw];
-        const half4 x0 = lds_tr4(base);
-        const half4 x1 = lds_tr4(base + 4 * RS);
-        return half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-      });
-    };
-    u32x4v pre0[NLD];
-    u32x4v pre1[PF == 2 ? NLD : 1];
-    if (nch > 0) fetch(pre0, 0);
-    __syncthreads();  // sq1, sp, salpha, srescale, szero initialised
-    if constexpr (PF == 2) {
-      if (nch > 1) fetch(pre1, 1);
-      for (int chi = 0; chi < nch; chi += 2) {
-        step(pre0, chi);
-        if (chi + 1 < nch) step(pre1, chi + 1);
-      }
-    } else {
-      for (int chi = 0; chi < nch; ++chi) step(pre0, chi);
-    }
+    for (int chi = 0; chi < nch; ++chi) step(pre0, chi);
   }
 
   // partials of this (row, split)
@@ -1037,7 +986,7 @@ int xattn_small_rows() {
 template <int D, int HT, int NS>
 void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T, int H, int S, int CH, float* z,
                  float* ml, int R, hipStream_t st) {
-  if constexpr ((D / 8) % 32 == 0 && !WA_XATTN_NW4)
+  if constexpr ((D / 8) % 32 == 0)
     hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z, ml, R);
   else
     hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 4, 1>), g, dim3(256), 0, st, qt, enc, Tq, T, H, S, CH, z, ml, R);
@@ -1137,11 +1086,6 @@ hipError_t launch_wv_pack(const uint8_t* wv, int H, int D, uint32_t* out, hipStr
 hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, const uint32_t* wvp, const float* bv,
                         int wtype, const _Float16* enc, int B, int Tq, int T, int H, int D, _Float16* qt, float* part,
                         _Float16* tiled, int ns, hipStream_t st) {
-  static const int skipb = [] {  // TEMPORARY removal ablation: 256 q, 512 main, 1024 out (Tq == 1 only)
-    const char* e = getenv("WA_SKIP");
-    return e ? atoi(e) : 0;
-  }();
-  const int sk = Tq == 1 ? skipb : 0;
   const int R = B * Tq;
   const int HT = (H + 15) / 16, HP = HT * 16;
   if (D != H * 64 || D % 128 != 0 || D > kMaxD || H > 20) return hipErrorInvalidValue;
@@ -1152,8 +1096,7 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   // qt = Wk^T q / 8
   const dim3 gq(H, D / 64, (R + 31) / 32);
 #define WA_XQ(NS_, WK_) hipLaunchKernelGGL((xattn_q_mfma_kernel<NS_, WK_>), gq, dim3(128), 0, st, q, R, D, wk, HP, qt)
-  if (sk & 256) {
-  } else if (wtype == kWtQ4) {
+  if (wtype == kWtQ4) {
     if (ns == 2) WA_XQ(2, kWtQ4); else WA_XQ(1, kWtQ4);
   } else {
     if (ns == 2) WA_XQ(2, kWtF16); else WA_XQ(1, kWtF16);
@@ -1164,8 +1107,7 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   const bool small = R <= xattn_small_rows() && p.ch <= kSmallMaxCH;
   float* scratch = part + ((size_t)R * p.splits * H * ((size_t)D + 2) + (size_t)R * H * D + 3) / 4 * 4;
 #define WA_XMAIN(DD, HH)                                                                   \
-  if (sk & 512) {                                                                          \
-  } else if (D == DD && HT == HH) {                                                        \
+  if (D == DD && HT == HH) {                                                               \
     if (small) {                                                                           \
       if (ns == 2)                                                                         \
         launch_small<DD, HH, 2>(R, Tq, T, H, p, qt, enc, z, ml, scratch, st);              \
@@ -1184,8 +1126,7 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   return hipErrorInvalidValue;
 #undef WA_XMAIN
   // merge the splits and project with Wv into the output projection's operand
-  if (sk & 1024) {
-  } else if (wtype == kWtQ4) {
+  if (wtype == kWtQ4) {
     if (ns == 2)
       launch_out<2, kWtQ4>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, st, small);
     else
