@@ -460,6 +460,141 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
   return hipGetLastError();
 }
 
+// ------------------------- cross-attention over cached K / V (few clips) --
+// The reference's own formulation (attention.rs:177-206 forward_init_cache:
+// K = enc Wk^T, V = enc Wv^T + bv cached per layer; :208-236 / 243-298
+// forward_with_cache: softmax(q K^T / 8) V), for decode groups of a few
+// clips: there the step is a latency chain, and one GEMV launch over the
+// cached K / V (f32, head-major [clip][head][T][64], written by the
+// head-major Q4 GEMM after the encoder) replaces the four launches of the
+// cache-free form (wa_xattn.hip).  Products are f32 x f32 (exact), sums and
+// softmax f32, as the reference's.
+//
+// Grid (H * S, B): the T keys of each (head, clip) are split over S
+// workgroups (S from T only: a clip's bits do not depend on its batch).
+// Each publishes (o[64], m, l) per query write-through (sc1 stores); the
+// last arriver of the (clip, head), told by its counter ticket, merges the S
+// partials in split order (sc1 loads; MI355X_MICROARCH.md hand-off table,
+// row 1) and writes the A-tiled operand of the output projection.
+constexpr int kXkvMaxSplit = 16;
+constexpr int kXkvPart = 68;  // floats per (query) partial: o[64], m, l, pad
+
+int cross_attention_kv_splits(int T) {
+  const int s = (T + 95) / 96;  // <= 96 keys per split: <= 24 per wave, one 8-deep scan pass
+  return s < 1 ? 1 : (s > kXkvMaxSplit ? kXkvMaxSplit : s);
+}
+
+template <int NS, int TQ>
+__global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restrict__ q, const float* __restrict__ kc,
+                                                            const float* __restrict__ vc, int Tq_, int T, int H,
+                                                            int S, float* __restrict__ part,
+                                                            int* __restrict__ counters,
+                                                            _Float16* __restrict__ tiled) {
+  const int Tq = TQ == 1 ? 1 : Tq_;
+  __shared__ float wm[4][TQ], wl[4][TQ];
+  __shared__ float wo[4][TQ][64];
+  __shared__ int last_flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int head = blockIdx.x / S, split = blockIdx.x - head * S, b = blockIdx.y;
+  const int D = H * 64;
+  const int sub = lane & 15, grp = lane >> 4;
+  floatx4 qv[TQ];
+#pragma unroll
+  for (int t = 0; t < TQ; ++t)
+    qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(q + (size_t)(b * Tq + t) * D + head * 64 + sub * 4) * kEaQScale
+                   : floatx4{0.f, 0.f, 0.f, 0.f};
+  const int per_split = (T + S - 1) / S;
+  const int s0 = min(T, split * per_split), s1 = min(T, s0 + per_split);
+  const int per_wave = (s1 - s0 + 3) / 4;
+  const int k0 = min(s1, s0 + wave * per_wave), k1 = min(s1, k0 + per_wave);
+  const size_t hofs = ((size_t)b * H + head) * T * 64 + sub * 4;
+  const float* kb = kc + hofs;
+  const float* vb = vc + hofs;
+  float m[TQ], l[TQ];
+  floatx4 o[TQ];
+  attn_scan<TQ, 8>(
+      qv, Tq, k0, k1, grp,
+      [&](int j, const float*& kp, const float*& vp) {
+        kp = kb + (size_t)j * 64;
+        vp = vb + (size_t)j * 64;
+      },
+      [](int, int) { return true; }, m, l, o);
+  float mn, ls, os;
+  attn_merge<TQ>(Tq, wave, lane, m, l, o, wm, wl, wo, mn, ls, os);
+  if (S > 1) {
+    typedef __attribute__((address_space(1))) float gfloat;
+    typedef __attribute__((address_space(1))) int gint;
+    const size_t bh = (size_t)b * H + head;
+    if (wave < Tq) {  // this split's partial, write-through
+      gfloat* pp = (gfloat*)(part + ((bh * S + split) * 4 + wave) * kXkvPart);
+      __hip_atomic_store(pp + lane, os, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_store(pp + 64, mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 1) __hip_atomic_store(pp + 65, ls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the ticket
+    __syncthreads();
+    if (tid == 0) {
+      const int prev = __hip_atomic_fetch_add((gint*)(counters + bh), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_flag = prev == S - 1;
+      if (prev == S - 1) __hip_atomic_store((gint*)(counters + bh), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last_flag || wave >= Tq) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: the loads stay below the ticket
+    // merge the S partials in split order (sc1 loads of sc1-stored bytes)
+    float po[kXkvMaxSplit], pm[kXkvMaxSplit], pl[kXkvMaxSplit];
+#pragma unroll
+    for (int sp = 0; sp < kXkvMaxSplit; ++sp) {
+      if (sp < S) {
+        gfloat* pp = (gfloat*)(part + ((bh * S + sp) * 4 + wave) * kXkvPart);
+        po[sp] = __hip_atomic_load(pp + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pm[sp] = __hip_atomic_load(pp + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pl[sp] = __hip_atomic_load(pp + 65, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    mn = -INFINITY;
+#pragma unroll
+    for (int sp = 0; sp < kXkvMaxSplit; ++sp)
+      if (sp < S) mn = fmaxf(mn, pm[sp]);
+    ls = 0.0f;
+    os = 0.0f;
+#pragma unroll
+    for (int sp = 0; sp < kXkvMaxSplit; ++sp) {
+      if (sp < S) {
+        const float a = pm[sp] == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(pm[sp] - mn);
+        ls += pl[sp] * a;
+        os += po[sp] * a;
+      }
+    }
+  }
+  if (wave < Tq) {
+    const int t = wave;
+    const float val = os / ls;
+    const float v1 = __shfl_down(val, 1, 64), v2 = __shfl_down(val, 2, 64), v3 = __shfl_down(val, 3, 64);
+    if ((lane & 3) == 0) atile_store4<NS>(tiled, b * Tq + t, head * 64 + lane, kbp_of(D), val, v1, v2, v3);
+  }
+}
+
+size_t cross_attention_kv_part_floats(int B, int H, int T) {
+  return (size_t)B * H * cross_attention_kv_splits(T) * 4 * kXkvPart;
+}
+
+hipError_t launch_cross_attention_kv(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
+                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st) {
+  if (Tq < 1 || Tq > 4 || B < 1 || T < 1 || H < 1) return hipErrorInvalidValue;
+  const int S = cross_attention_kv_splits(T);
+  const dim3 grid(H * S, B), block(256);
+#define WA_XKV(NS_, TQ_) \
+  hipLaunchKernelGGL((cross_attn_kv_kernel<NS_, TQ_>), grid, block, 0, st, q, k, v, Tq, T, H, S, part, counters, tiled)
+  if (ns == 2) {
+    if (Tq == 1) WA_XKV(2, 1); else WA_XKV(2, 4);
+  } else {
+    if (Tq == 1) WA_XKV(1, 1); else WA_XKV(1, 4);
+  }
+#undef WA_XKV
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------ conv + GELU --
 // out[b, t, n] = gelu(bias[n] + sum_{kk, c} in(b, c, t*S + kk - 1) W[n, c, kk])
 // (+ pos[t, n]).  GEMM view: rows (b, t), cols n, K = 3C (k = kk*C + c, the

@@ -30,6 +30,17 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
                                          int ctx, const DecodeState* state, int kv_len_host, _Float16* tiled,
                                          int ns, hipStream_t st);
 
+// Cross-attention over cached K / V (attention.rs:177-236, the reference's
+// form; used for decode groups of a few clips): q [B*Tq, D] f32, k / v
+// head-major [B][H][T][64] f32 (wq4_gemm_tiled_headmajor of the encoder
+// output), Tq <= 4; part: cross_attention_kv_part_floats floats, counters:
+// B * H ints zeroed once (re-armed by the kernel).  Writes the A-tiled
+// operand of the output projection.
+int cross_attention_kv_splits(int T);
+size_t cross_attention_kv_part_floats(int B, int H, int T);
+hipError_t launch_cross_attention_kv(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
+                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st);
+
 // Cross-attention over the encoder output (wa_xattn.hip; attention.rs:
 // 204-298 restated without K/V caches): q [B*Tq, D] f32 (rows b*Tq + i),
 // wk / wv: the layer's raw key / value weights [D, D] (wtype: Q4_0 blocks or

@@ -157,6 +157,11 @@ struct DecLayer {
   uint8_t *ck_raw = nullptr, *cv_raw = nullptr;
   uint32_t* cv_p = nullptr;  // Q4_0: cv_raw in the projection's lane order (wa::launch_wv_pack)
   float *cache_k, *cache_v;
+  // few-clip decode groups (wa_model::kv_clips): the reference's per-layer
+  // cross K / V caches, head-major [clip][head][T][64] f32, written by the
+  // head-major GEMMs of ck / cv over the encoder output (cross_kv_forward)
+  wq4_tensor *ck = nullptr, *cv = nullptr;
+  float *xk = nullptr, *xv = nullptr;
 };
 
 // One decode group: a contiguous range of clips [b0, b0 + nb) decoded on its
@@ -175,6 +180,8 @@ struct DecGroup {
   int *prompt_tok, *next_tok, *tokens, *ntok, *done;
   _Float16* xqt;    // cross-attention Wk^T q operands [rows][ns][16*ceil(H/16)][D]
   float* xattn_part;  // cross-attention split partials (Z, max, sum)
+  float* xkv_part;    // cross-attention over cached K / V: split partials
+  int* xkv_ctr;       //   and the per-(clip, head) arrival counters
   _Float16* atd_ln;   // LayerNorm fold: A-tiled x * gamma of the next LayerNorm
   float* ln_stats;    //                 its per (row, 32-column tile) mean / M2
   _Float16* hid_t;    // fused logits + argmax: the final LN, A-tiled (m-tile 0)
@@ -214,6 +221,12 @@ struct wa_model {
   std::vector<DecGroup> groups;
   int wtype = 0;     // linear weights: 0 Q4_0, 1 f16 (BASELINE config 5)
   int kv_batch = 0;  // clips of the last encoder pass (enc_planes valid for [0, kv_batch))
+  // Cross K / V caches for transcribes of at most kv_clips clips (their
+  // decode steps are launch-latency chains: one GEMV launch over the caches
+  // replaces the cache-free cross-attention's four, wa_kernels.hip);
+  // kv_valid: the last encoder pass filled them for its kv_batch clips.
+  int kv_clips = 0;
+  bool kv_valid = false;
   hipStream_t own_stream = nullptr;  // encoder / encoder planes (graph capture needs a non-null stream)
   float timings[5] = {0, 0, 0, 0, 0};
   // decode-step logit trace (wa_transcribe_trace; null otherwise): device
@@ -257,7 +270,7 @@ struct wa_model {
     for (auto& l : enc)
       for (wq4_tensor* t : {l.qkv, l.out, l.fc1, l.fc2}) wq4_tensor_destroy(t);
     for (auto& l : dec)
-      for (wq4_tensor* t : {l.qkv, l.out, l.cq, l.cout, l.fc1, l.fc2}) wq4_tensor_destroy(t);
+      for (wq4_tensor* t : {l.qkv, l.out, l.cq, l.cout, l.fc1, l.fc2, l.ck, l.cv}) wq4_tensor_destroy(t);
   }
 };
 
@@ -529,6 +542,10 @@ wq4_status build_model(wa_model* m, Source& src) {
       m->bytes += nw * 4;
     }
     L.cv_b = B.bias_cat({p + ".cross_attn.value.bias"}, Dt);
+    if (m->kv_clips > 0) {  // the cache GEMMs run at encoder row counts only: no decode-step copy
+      L.ck = B.q4({p + ".cross_attn.key.weight"}, {Dt}, D, false);
+      L.cv = B.q4({p + ".cross_attn.value.weight"}, {Dt}, D, false);
+    }
     L.cout = B.q4({p + ".cross_attn.out.weight"}, {Dt}, Dt);
     L.cout_b = B.vec(p + ".cross_attn.out.bias", Dt, -0.02f, 0.02f);
     L.ln3_w = B.vec(p + ".mlp_ln.weight", Dt, 0.9f, 1.1f);
@@ -619,6 +636,11 @@ wq4_status alloc_activations(wa_model* m) {
   for (auto& L : m->dec) {
     L.cache_k = f32((int64_t)B * c.n_text_ctx * Dt);
     L.cache_v = f32((int64_t)B * c.n_text_ctx * Dt);
+    if (m->kv_clips > 0) {
+      L.xk = f32((int64_t)m->kv_clips * T * Dt);
+      L.xv = f32((int64_t)m->kv_clips * T * Dt);
+      if (!L.xk || !L.xv) return fail(WQ4_ENOMEM, "cross K/V cache allocation failed");
+    }
   }
   // f16-pair tied embedding for the decode step's fused logits + pick,
   // fragment-tiled (1 KiB contiguous per load instruction)
@@ -648,6 +670,9 @@ wq4_status alloc_activations(wa_model* m) {
     g.done = d.alloc<int>(B);
     g.state = d.alloc<wa::DecodeState>(1);
     g.xattn_part = f32((int64_t)xpart);
+    const int kvc = std::max(1, m->kv_clips);
+    g.xkv_part = f32((int64_t)wa::cross_attention_kv_part_floats(kvc, c.n_text_head, T));
+    g.xkv_ctr = d.alloc<int>((size_t)kvc * c.n_text_head);
     g.xqt = d.alloc<_Float16>((size_t)rdec * m->ns * HP * Dt);
     g.atd_ln = tiled(rdec, Dt);
     g.ln_stats = f32(rdec * (Dt / 16) * 2);  // per 16-column tile (the decode-step GEMM)
@@ -659,8 +684,10 @@ wq4_status alloc_activations(wa_model* m) {
     for (void* p : {(void*)g.xd, (void*)g.qkvd, (void*)g.qd, (void*)g.hid, (void*)g.logits, (void*)g.atd_dec,
                     (void*)g.atf_dec, (void*)g.prompt_tok, (void*)g.next_tok, (void*)g.tokens, (void*)g.ntok,
                     (void*)g.done, (void*)g.state, (void*)g.xattn_part, (void*)g.xqt, (void*)g.lg_val,
-                    (void*)g.lg_idx, (void*)g.lg_ctr, (void*)g.atd_ln, (void*)g.ln_stats, (void*)g.hid_t})
+                    (void*)g.lg_idx, (void*)g.lg_ctr, (void*)g.atd_ln, (void*)g.ln_stats, (void*)g.hid_t,
+                    (void*)g.xkv_part, (void*)g.xkv_ctr})
       if (!p) return fail(WQ4_ENOMEM, "decode-group allocation failed");
+    WA_HIP(hipMemset(g.xkv_ctr, 0, (size_t)kvc * c.n_text_head * sizeof(int)));
     WA_HIP(hipMemset(g.atd_ln, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
     WA_HIP(hipMemset(g.hid_t, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));  // padded clips stay 0
     WA_HIP(hipMemset(g.lg_ctr, 0, sizeof(int)));
@@ -771,10 +798,26 @@ wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st,
 // K = enc Wk^T and V = enc Wv^T per layer (attention.rs:177-206
 // forward_init_cache); here one copy of encoder_out as f16 planes serves all
 // layers (wa_xattn.hip).
+// Transcribes of at most kv_clips clips also get the reference's own
+// per-layer caches, K = enc Wk^T and V = enc Wv^T + bv, head-major (the
+// few-clip decode reads them: launch_cross_attention_kv).
 wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st) {
-  const int64_t rows = (int64_t)B * m->cfg.n_audio_ctx;
+  const Config& c = m->cfg;
+  const int64_t rows = (int64_t)B * c.n_audio_ctx;
   m->kv_batch = B;
-  WA_HIP(wa::launch_enc_planes(m->enc_f32, rows, m->cfg.n_audio_state, m->ns, m->enc_planes, st));
+  WA_HIP(wa::launch_enc_planes(m->enc_f32, rows, c.n_audio_state, m->ns, m->enc_planes, st));
+  m->kv_valid = false;
+  if (B <= m->kv_clips) {
+    // ln_post again, as the GEMMs' A-tiled operand (m->x still holds its input)
+    WA_WQ4(wq4_layernorm(m->x, m->lnp_w, m->lnp_b, rows, c.n_audio_state, m->prec, m->at_d, nullptr, st));
+    for (DecLayer& L : m->dec) {
+      WA_WQ4(wq4_gemm_tiled_headmajor(L.ck, nullptr, m->at_d, L.xk, rows, c.n_audio_ctx, c.n_text_state, m->prec, 0,
+                                      st));
+      WA_WQ4(wq4_gemm_tiled_headmajor(L.cv, L.cv_b, m->at_d, L.xv, rows, c.n_audio_ctx, c.n_text_state, m->prec, 0,
+                                      st));
+    }
+    m->kv_valid = true;
+  }
   return WQ4_OK;
 }
 
@@ -844,8 +887,14 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
       WA_WQ4(wq4_layernorm(g.xd, L.ln2_w, L.ln2_b, rows, D, m->prec, g.atd_dec, nullptr, st));
       WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, g.atd_dec, nullptr, g.qd, nullptr, rows, 0u, m->prec, 2, st));
     }
-    WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, Tq, T, H, D, g.xqt, g.xattn_part,
-                            g.atd_dec, m->ns, st));
+    if (m->kv_valid) {  // few clips: one GEMV launch over the cached K / V
+      const size_t kofs = (size_t)g.b0 * T * D;
+      WA_HIP(wa::launch_cross_attention_kv(g.qd, L.xk + kofs, L.xv + kofs, B, Tq, T, H, g.xkv_part, g.xkv_ctr,
+                                           g.atd_dec, m->ns, st));
+    } else {
+      WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, Tq, T, H, D, g.xqt,
+                              g.xattn_part, g.atd_dec, m->ns, st));
+    }
     if (fold) {
       const wq4_ln_fold prod3{L.ln3_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
       WA_WQ4(wq4_gemm_tiled_lnfold(L.cout, L.cout_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL,
@@ -953,7 +1002,8 @@ wq4_status prompt_group(wa_model* m, DecGroup& g, int lang_token, hipStream_t st
 wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
   // everything the captured step bakes in: the clip range (self-KV and
   // encoder-plane offsets), the EOT mode and the trace buffers
-  const int64_t key = (((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0);
+  const int64_t key =
+      ((((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0)) * 2 + (m->kv_valid ? 1 : 0);
   if (g.graph && g.graph_key == key) return WQ4_OK;
   if (g.graph) {
     (void)hipGraphExecDestroy(g.graph);
@@ -971,6 +1021,16 @@ wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
   if (ce != hipSuccess) return fail(WQ4_EHIP, std::string("graph instantiate: ") + hipGetErrorString(ce));
   g.graph_key = key;
   return WQ4_OK;
+}
+
+// Clips up to which a transcribe decodes over cross K / V caches
+// (WA_XATTN_KV_CLIPS overrides; 0 = never): 4, measured in DESIGN.md §4.
+int kv_clips_for(int max_batch) {
+  static const int lim = [] {
+    const char* e = getenv("WA_XATTN_KV_CLIPS");
+    return e ? std::max(0, atoi(e)) : 4;
+  }();
+  return std::min(lim, max_batch);
 }
 
 // Number of decode groups for a batch (WA_DECODE_GROUPS overrides).
@@ -1013,6 +1073,7 @@ wq4_status wa_model_create_synthetic_ex(int device, int variant, uint64_t seed, 
   m->prec = prec;
   m->ns = prec == WQ4_PREC_F16 ? 1 : 2;
   m->bmax = max_batch;
+  m->kv_clips = kv_clips_for(max_batch);
   m->wtype = weight_type;
   SynthSource src(seed);
   wq4_status s = build_model(m.get(), src);
@@ -1048,6 +1109,7 @@ wq4_status wa_model_create_from_gguf(int device, const char* path, int variant, 
   m->prec = prec;
   m->ns = prec == WQ4_PREC_F16 ? 1 : 2;
   m->bmax = max_batch;
+  m->kv_clips = kv_clips_for(max_batch);
   const wa::GgufTensor* probe = file.find("encoder.blocks.0.attn.query.weight");
   m->wtype = probe && probe->type == wa::kGgmlF16 ? 1 : 0;  // an F16 checkpoint (config 5)
   GgufSource src(file);
