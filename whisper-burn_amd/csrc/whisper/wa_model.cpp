@@ -221,12 +221,15 @@ struct wa_model {
   std::vector<DecGroup> groups;
   int wtype = 0;     // linear weights: 0 Q4_0, 1 f16 (BASELINE config 5)
   int kv_batch = 0;  // clips of the last encoder pass (enc_planes valid for [0, kv_batch))
-  // Cross K / V caches for transcribes of at most kv_clips clips (their
-  // decode steps are launch-latency chains: one GEMV launch over the caches
-  // replaces the cache-free cross-attention's four, wa_kernels.hip);
-  // kv_valid: the last encoder pass filled them for its kv_batch clips.
-  int kv_clips = 0;
-  bool kv_valid = false;
+  // Cross K / V caches (capacity kv_clips clips) for transcribes of at most
+  // kv_small clips -- their decode steps are launch-latency chains: one GEMV
+  // launch over the caches replaces the cache-free cross-attention's four,
+  // wa_kernels.hip -- or, for larger ones, the first kv_prefix clips (A/B
+  // knob).  kv_n: clips [0, kv_n) of the last encoder pass have caches; a
+  // decode group entirely inside them reads the caches.
+  int kv_clips = 0, kv_small = 0, kv_prefix = 0;
+  int kv_n = 0;
+  bool group_kv(const DecGroup& g) const { return g.nb > 0 && g.b0 + g.nb <= kv_n; }
   hipStream_t own_stream = nullptr;  // encoder / encoder planes (graph capture needs a non-null stream)
   float timings[5] = {0, 0, 0, 0, 0};
   // decode-step logit trace (wa_transcribe_trace; null otherwise): device
@@ -806,17 +809,18 @@ wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st) {
   const int64_t rows = (int64_t)B * c.n_audio_ctx;
   m->kv_batch = B;
   WA_HIP(wa::launch_enc_planes(m->enc_f32, rows, c.n_audio_state, m->ns, m->enc_planes, st));
-  m->kv_valid = false;
-  if (B <= m->kv_clips) {
-    // ln_post again, as the GEMMs' A-tiled operand (m->x still holds its input)
-    WA_WQ4(wq4_layernorm(m->x, m->lnp_w, m->lnp_b, rows, c.n_audio_state, m->prec, m->at_d, nullptr, st));
+  m->kv_n = std::min(B <= m->kv_small ? B : m->kv_prefix, m->kv_clips);
+  if (m->kv_n > 0) {
+    // ln_post again, as the GEMMs' A-tiled operand (m->x still holds its
+    // input); the caches of clips [0, kv_n): a prefix of the rows
+    const int64_t kv_rows = (int64_t)m->kv_n * c.n_audio_ctx;
+    WA_WQ4(wq4_layernorm(m->x, m->lnp_w, m->lnp_b, kv_rows, c.n_audio_state, m->prec, m->at_d, nullptr, st));
     for (DecLayer& L : m->dec) {
-      WA_WQ4(wq4_gemm_tiled_headmajor(L.ck, nullptr, m->at_d, L.xk, rows, c.n_audio_ctx, c.n_text_state, m->prec, 0,
-                                      st));
-      WA_WQ4(wq4_gemm_tiled_headmajor(L.cv, L.cv_b, m->at_d, L.xv, rows, c.n_audio_ctx, c.n_text_state, m->prec, 0,
-                                      st));
+      WA_WQ4(wq4_gemm_tiled_headmajor(L.ck, nullptr, m->at_d, L.xk, kv_rows, c.n_audio_ctx, c.n_text_state, m->prec,
+                                      0, st));
+      WA_WQ4(wq4_gemm_tiled_headmajor(L.cv, L.cv_b, m->at_d, L.xv, kv_rows, c.n_audio_ctx, c.n_text_state, m->prec,
+                                      0, st));
     }
-    m->kv_valid = true;
   }
   return WQ4_OK;
 }
@@ -887,7 +891,7 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
       WA_WQ4(wq4_layernorm(g.xd, L.ln2_w, L.ln2_b, rows, D, m->prec, g.atd_dec, nullptr, st));
       WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, g.atd_dec, nullptr, g.qd, nullptr, rows, 0u, m->prec, 2, st));
     }
-    if (m->kv_valid) {  // few clips: one GEMV launch over the cached K / V
+    if (m->group_kv(g)) {  // few clips: one GEMV launch over the cached K / V
       const size_t kofs = (size_t)g.b0 * T * D;
       WA_HIP(wa::launch_cross_attention_kv(g.qd, L.xk + kofs, L.xv + kofs, B, Tq, T, H, g.xkv_part, g.xkv_ctr,
                                            g.atd_dec, m->ns, st));
@@ -1003,7 +1007,8 @@ wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
   // everything the captured step bakes in: the clip range (self-KV and
   // encoder-plane offsets), the EOT mode and the trace buffers
   const int64_t key =
-      ((((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0)) * 2 + (m->kv_valid ? 1 : 0);
+      ((((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0)) * 2 +
+      (m->group_kv(g) ? 1 : 0);
   if (g.graph && g.graph_key == key) return WQ4_OK;
   if (g.graph) {
     (void)hipGraphExecDestroy(g.graph);
@@ -1024,13 +1029,21 @@ wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
 }
 
 // Clips up to which a transcribe decodes over cross K / V caches
-// (WA_XATTN_KV_CLIPS overrides; 0 = never): 4, measured in DESIGN.md §4.
-int kv_clips_for(int max_batch) {
-  static const int lim = [] {
+// (WA_XATTN_KV_CLIPS overrides; 0 = never; measured in DESIGN.md §4), and
+// WA_XATTN_KV_PREFIX: larger transcribes give their first that many clips
+// caches too (A/B knob; 0 by default).
+void kv_config(wa_model* m, int max_batch) {
+  static const int small = [] {
     const char* e = getenv("WA_XATTN_KV_CLIPS");
-    return e ? std::max(0, atoi(e)) : 4;
+    return e ? std::max(0, atoi(e)) : 8;
   }();
-  return std::min(lim, max_batch);
+  static const int prefix = [] {
+    const char* e = getenv("WA_XATTN_KV_PREFIX");
+    return e ? std::max(0, atoi(e)) : 0;
+  }();
+  m->kv_small = std::min(small, max_batch);
+  m->kv_prefix = std::min(prefix, max_batch);
+  m->kv_clips = std::max(m->kv_small, m->kv_prefix);
 }
 
 // Number of decode groups for a batch (WA_DECODE_GROUPS overrides).
@@ -1073,7 +1086,7 @@ wq4_status wa_model_create_synthetic_ex(int device, int variant, uint64_t seed, 
   m->prec = prec;
   m->ns = prec == WQ4_PREC_F16 ? 1 : 2;
   m->bmax = max_batch;
-  m->kv_clips = kv_clips_for(max_batch);
+  kv_config(m.get(), max_batch);
   m->wtype = weight_type;
   SynthSource src(seed);
   wq4_status s = build_model(m.get(), src);
@@ -1109,7 +1122,7 @@ wq4_status wa_model_create_from_gguf(int device, const char* path, int variant, 
   m->prec = prec;
   m->ns = prec == WQ4_PREC_F16 ? 1 : 2;
   m->bmax = max_batch;
-  m->kv_clips = kv_clips_for(max_batch);
+  kv_config(m.get(), max_batch);
   const wa::GgufTensor* probe = file.find("encoder.blocks.0.attn.query.weight");
   m->wtype = probe && probe->type == wa::kGgmlF16 ? 1 : 0;  // an F16 checkpoint (config 5)
   GgufSource src(file);

@@ -12,6 +12,7 @@
 
 #include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -42,7 +43,13 @@ namespace {
 
 thread_local std::string g_err;
 std::atomic<int> g_prec{WQ4_PREC_F16X2};
-std::atomic<int> g_policy{0};
+// WQ4_KERNEL_POLICY initialises it (A/B runs of whole programs, e.g. bench.py);
+// wq4_set_kernel_policy changes it at run time.
+std::atomic<int> g_policy{[] {
+  const char* env = getenv("WQ4_KERNEL_POLICY");
+  const int v = env ? atoi(env) : 0;
+  return v >= 0 && v <= 3 ? v : 0;
+}()};
 
 wq4_status fail(wq4_status s, const std::string& msg) {
   g_err = msg;

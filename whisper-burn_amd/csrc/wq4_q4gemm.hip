@@ -479,6 +479,16 @@ __host__ __device__ constexpr size_t decode_lds_bytes_dev(int w) {
 #ifndef WQ4_DIAG
 #define WQ4_DIAG 0
 #endif
+// Q4_0 weights at f16x2: block-scaled products (1, the product) -- per Q4
+// block t = MFMA(x_hi, q0) + MFMA(x_lo, q0) + MFMA(x_hi, q1) + MFMA(x_lo, q1)
+// (q - 8 exact in f16, f32 accumulation), then acc = fma(t, d', acc) for the
+// accumulator rows that hold real rows only -- the arithmetic of the prefill
+// and decode-step kernels: two MFMAs per 16 k and no weight-side split,
+// where B = (q - 8) d' = B_hi + B_lo (0, the round-2 form) needs three
+// MFMAs and the split's VALU.  Compile-time switch for A/B builds.
+#ifndef WQ4_DECODE_BS
+#define WQ4_DECODE_BS 1
+#endif
 template <int NS, int EPI, int PER, int MT, int W, int WK, bool LNA = false>
 __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* __restrict__ nib,
                                                               const uint32_t* __restrict__ sc,
@@ -691,8 +701,33 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
       acc0[i] = 0.0f;
       acc1[i] = 0.0f;
     }
+    // block-scaled form: accumulator elements j < jmax hold this m-tile's
+    // real rows (element j: row (j & 3) + 8 (j >> 2) + 4 h); the rest stay 0
+    // and are never stored.  Wave-uniform, and a row's arithmetic does not
+    // depend on it.
+    const int mrows = e.m - (mt0 + mt) * 32;
+    const int jmax = mrows <= 8 ? 4 : mrows <= 16 ? 8 : mrows <= 24 ? 12 : 16;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
+      if constexpr (WQ4_DECODE_BS && WK == kWeightsQ4 && NS == 2) {
+        if (kDiag != 1 && i < cnt) {
+#pragma unroll
+          for (int blk = 0; blk < 2; ++blk) {
+            const half8 q0 = deq8(br[i][0][blk * 2 + 0]);  // exact q - 8, k-half 0 / 1
+            const half8 q1 = deq8(br[i][0][blk * 2 + 1]);
+            const float d = (float)__builtin_bit_cast(_Float16, (uint16_t)(blk ? (bs[i] >> 16) : (bs[i] & 0xffffu)));
+            floatx16 t = mfma32(a[mt][i][blk][0][0], q0, floatx16{});
+            t = mfma32(a[mt][i][blk][0][1], q0, t);
+            t = mfma32(a[mt][i][blk][1][0], q1, t);
+            t = mfma32(a[mt][i][blk][1][1], q1, t);
+            floatx16& acc = blk ? acc1 : acc0;  // two chains: even / odd blocks
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+              if (j < jmax) acc[j] = fmaf(t[j], d, acc[j]);
+          }
+        }
+        continue;
+      }
       if (kDiag != 1 && i < cnt) {
 #pragma unroll
         for (int blk = 0; blk < 2; ++blk) {
