@@ -395,11 +395,15 @@ def main() -> None:
         xa = probe["cross_attention"]
         xa_gbs = xa["bytes"] / (xa["us"] * 1e-6) * 1e-9
         groups = -(-B // group_rows)
-        ig = in_graph_xattn(group_rows, cfg["n_text_head"], cfg["n_text_state"], workload)
+        kv = xa["kv_cache"]  # few clips: the GEMV over the cached cross K / V (one launch)
+        ig = None if kv else in_graph_xattn(group_rows, cfg["n_text_head"], cfg["n_text_state"], workload)
+        xa_kernel = ("cross-attention over the cached cross K / V: cross_attn_kv_kernel" if kv else
+                     "cross-attention over the encoder output: xattn_q + xattn_main + xattn_out")
         roof_xa = {"bound": "hbm", "achieved": round(xa_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                    "frac": round(xa_gbs / PEAK_HBM_GBS, 4),
-                   "traffic": pmc_traffic_xattn_probe(group_rows, cfg["n_text_head"], cfg["n_text_state"], workload),
-                   "kernel": f"cross-attention over the encoder output: xattn_q + xattn_main + xattn_out "
+                   "traffic": None if kv else pmc_traffic_xattn_probe(group_rows, cfg["n_text_head"],
+                                                                      cfg["n_text_state"], workload),
+                   "kernel": f"{xa_kernel} "
                              f"(decode step, Tq = 1, {group_rows} clips per launch = one of {groups} decode groups)",
                    "avg_us": round(xa["us"], 2), "bytes_per_launch": xa["bytes"],
                    "in_graph_avg_us": None if ig is None else round(ig, 2),

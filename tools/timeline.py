@@ -22,7 +22,7 @@ for r in rows:
         name = f"{name}[{r.get('Grid_Size_X', r.get('Grid_Size', ''))}]"
     K.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Queue_Id", "0"), name))
 K.sort()
-dec = re.compile(r"xattn|dec_self|q4_gemm_decode|skinny_gemm|logits_argmax|embed_fold|bookkeep")
+dec = re.compile(r"xattn|cross_attn_kv|dec_self|q4_gemm_decode|skinny_gemm|logits_argmax|embed_fold|bookkeep")
 D = [k for k in K if dec.search(k[3])]
 if not D:
     sys.exit("no decode kernels")

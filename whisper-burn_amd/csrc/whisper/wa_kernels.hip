@@ -476,11 +476,19 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
 // last arriver of the (clip, head), told by its counter ticket, merges the S
 // partials in split order (sc1 loads; MI355X_MICROARCH.md hand-off table,
 // row 1) and writes the A-tiled operand of the output projection.
-constexpr int kXkvMaxSplit = 16;
+constexpr int kXkvMaxSplit = 32;
 constexpr int kXkvPart = 68;  // floats per (query) partial: o[64], m, l, pad
 
 int cross_attention_kv_splits(int T) {
-  const int s = (T + 95) / 96;  // <= 96 keys per split: <= 24 per wave, one 8-deep scan pass
+  static const int keys = [] {  // keys per split (A/B knob WA_XKV_KEYS; a function of T only either way)
+    const char* e = getenv("WA_XKV_KEYS");
+    const int v = e ? atoi(e) : 188;
+    return v >= 16 ? v : 188;
+  }();
+  // 188 (8 splits at T = 1500, <= 47 keys per wave: one 12-deep scan pass);
+  // measured at one clip (Large-V3, in the decode step): 9.2 us per launch
+  // vs 9.9 at 96 keys, 11.1 at 375, 13.4 at 48
+  const int s = (T + keys - 1) / keys;
   return s < 1 ? 1 : (s > kXkvMaxSplit ? kXkvMaxSplit : s);
 }
 
@@ -512,7 +520,7 @@ __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restr
   const float* vb = vc + hofs;
   float m[TQ], l[TQ];
   floatx4 o[TQ];
-  attn_scan<TQ, 8>(
+  attn_scan<TQ, TQ == 1 ? 12 : 8>(  // <= 48 keys per wave in flight at once (decode step)
       qv, Tq, k0, k1, grp,
       [&](int j, const float*& kp, const float*& vp) {
         kp = kb + (size_t)j * 64;

@@ -1436,20 +1436,31 @@ wq4_status wa_probe_kernels(wa_model* m, int n_clips, int iters, double* out) {
   WA_HIP(hipEventCreate(&a));
   WA_HIP(hipEventCreate(&b));
   float ms = 0.0f;
-  // cross-attention of one decode step (Tq = 1): streams every clip's encoder output
-  WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, 1, T, H, D, g.xqt, g.xattn_part,
-                          g.atd_dec, m->ns, st));
+  // cross-attention of one decode step (Tq = 1) in the form a decode group of
+  // n_clips clips runs: over the cached K / V (few clips) or streaming every
+  // clip's encoder output
+  g.b0 = 0;
+  g.nb = B;
+  const bool kv = m->group_kv(g);
+  auto xattn = [&]() -> hipError_t {
+    if (kv)
+      return wa::launch_cross_attention_kv(g.qd, L.xk, L.xv, B, 1, T, H, g.xkv_part, g.xkv_ctr, g.atd_dec, m->ns, st);
+    return wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, 1, T, H, D, g.xqt,
+                            g.xattn_part, g.atd_dec, m->ns, st);
+  };
+  WA_HIP(xattn());
   WA_HIP(hipEventRecord(a, st));
-  for (int i = 0; i < iters; ++i)
-    WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, 1, T, H, D, g.xqt, g.xattn_part,
-                            g.atd_dec, m->ns, st));
+  for (int i = 0; i < iters; ++i) WA_HIP(xattn());
   WA_HIP(hipEventRecord(b, st));
   WA_HIP(hipEventSynchronize(b));
   WA_HIP(hipEventElapsedTime(&ms, a, b));
   out[0] = ms * 1e3 / iters;
-  // algorithmic bytes: encoder output planes of every clip + Wk, Wv (raw) + q + output operand
+  // algorithmic bytes: the cached K and V (f32) of every clip, or the
+  // encoder output planes of every clip + Wk, Wv (raw); + q + output operand
   const double wbytes = m->wtype == 1 ? 2.0 * D * D * 2 : 2.0 * D * D * 18 / 32;
-  out[1] = (double)B * T * D * 2 * m->ns + wbytes + (double)B * D * (4 + 2 * m->ns);
+  out[1] = kv ? (double)B * T * D * 4 * 2 + (double)B * D * (4 + 2 * m->ns)
+              : (double)B * T * D * 2 * m->ns + wbytes + (double)B * D * (4 + 2 * m->ns);
+  out[5] = kv ? 1.0 : 0.0;
   // fc1 of one decode step (M = n_clips rows, decode kernel, GELU + tiled out)
   const int F = 4 * D;
   WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, g.atd_dec, nullptr, nullptr, g.atf_dec, B, WQ4_EPI_GELU | WQ4_EPI_TILED_OUT,

@@ -342,9 +342,9 @@ class WhisperModel:
 
     def probe_kernels(self, n_clips: int, iters: int = 20) -> dict:
         """HIP-event timing of single decode-step kernels (after transcribe)."""
-        buf = (ctypes.c_double * 5)()
+        buf = (ctypes.c_double * 6)()
         check(lib().wa_probe_kernels(self._h, n_clips, iters, buf))
-        return {"cross_attention": {"us": buf[0], "bytes": buf[1]},
+        return {"cross_attention": {"us": buf[0], "bytes": buf[1], "kv_cache": buf[5] != 0.0},
                 "decode_fc1": {"us": buf[2], "bytes": buf[3], "flops": buf[4]}}
 
     def encode(self, mel):
