@@ -32,10 +32,12 @@ constexpr int kEOT = 50257;
 constexpr float kEaQScale = 0.125f * 1.4426950408889634f;
 // Operand scales of the f16-pair MFMAs (the MFMAs flush f16 subnormal inputs,
 // wq4_device.hpp split_act): q / 8 (base 2), k and v enter as x * 2^5 (|x| <
-// 2047), the softmax weights p in (0, 1] as p * 2^15 (<= 32768 < 65504); the
-// scores come out x 2^10 and the output x 2^20 -- undone in f32, exactly.
+// 2047), the softmax weights p in (0, 2] (lazy reference maximum) as p * 2^14
+// (<= 32768 < 65504); the scores come out x 2^10 and the output x 2^19 --
+// undone in f32, exactly.
 constexpr float kQKScale = 32.0f, kSInv = 1.0f / 1024.0f;
-constexpr float kPScale = 32768.0f, kPVInv = 1.0f / (32768.0f * 32.0f);
+constexpr float kPScale = 16384.0f, kPVInv = 1.0f / (16384.0f * 32.0f);
+constexpr float kEaLazyMax = 1024.0f;  // 1.0 in base-2 units x 2^10 (the scores' operand scale)
 // the conv front-end: input x 2^4, weights x 2^10 (|w| < 64), product x 2^-14
 constexpr float kCvAScale = 16.0f, kCvBScale = 1024.0f, kCvInv = 1.0f / (16.0f * 1024.0f);
 // logits: hidden rows as GEMM activations (x 2^4), the f16-pair table x 2^8
@@ -85,14 +87,33 @@ __device__ __forceinline__ floatx16 ea_mfma(half8 a, half8 b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// Two split_f16 at once: hi = RNE(x) of both by one v_cvt_pk_f16_f32, the
+// exact remainders x - hi by one packed subtract, lo = their RNE -- five
+// instructions per pair where two split_f16 take eight; the same bits.
+typedef _Float16 ea_half2 __attribute__((ext_vector_type(2)));
+typedef float ea_float2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split2(float a, float b, ea_half2& hi, ea_half2& lo) {
+  hi = __builtin_convertvector((ea_float2){a, b}, ea_half2);
+  const ea_float2 r = (ea_float2){a, b} - __builtin_convertvector(hi, ea_float2);
+  lo = __builtin_convertvector(r, ea_half2);
+}
+
 constexpr int kEaKeys = 64;  // keys per LDS tile
 constexpr int kEaLd = 72;    // LDS row stride (halves)
 
+// Registers held to 128 (4 waves per SIMD: two 8-wave workgroups per CU,
+// one's staging beside the other's MFMAs); WA_EA_WAVES: A/B builds.
+#ifndef WA_EA_WAVES
+#define WA_EA_WAVES 4
+#endif
 template <int NS, int NW>
-__global__ __launch_bounds__(64 * NW) void encoder_attention_f16_kernel(const float* __restrict__ qkv, int T, int H,
-                                                                    _Float16* __restrict__ tiled) {
-  __shared__ __attribute__((aligned(16))) _Float16 kls[NS][kEaKeys * kEaLd];
-  __shared__ __attribute__((aligned(16))) _Float16 vls[NS][kEaKeys * kEaLd];
+__global__ __launch_bounds__(64 * NW, WA_EA_WAVES) void encoder_attention_f16_kernel(const float* __restrict__ qkv,
+                                                                                    int T, int H,
+                                                                                    _Float16* __restrict__ tiled) {
+  // two tile buffers: tile kt + 1 is staged into the other one while tile
+  // kt is read, one barrier per tile
+  __shared__ __attribute__((aligned(16))) _Float16 klsb[2][NS][kEaKeys * kEaLd];
+  __shared__ __attribute__((aligned(16))) _Float16 vlsb[2][NS][kEaKeys * kEaLd];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, lh = lane >> 5;
   const int head = blockIdx.y, b = blockIdx.z;
@@ -138,17 +159,23 @@ __global__ __launch_bounds__(64 * NW) void encoder_attention_f16_kernel(const fl
       vreg[i] = ok ? *reinterpret_cast<const floatx4*>(kr + D + 4 * i) : floatx4{0.f, 0.f, 0.f, 0.f};
     }
   };
-  auto stage = [&]() {
+  auto stage = [&](int buf) {
+    _Float16(*kls)[kEaKeys * kEaLd] = klsb[buf];
+    _Float16(*vls)[kEaKeys * kEaLd] = vlsb[buf];
     half8 kh[EPT / 8], kl[EPT / 8], vh[EPT / 8], vl[EPT / 8];
 #pragma unroll
-    for (int i = 0; i < EPT; ++i) {
-      _Float16 a, c;
-      split_f16(kreg[i >> 2][i & 3] * kQKScale, a, c);
-      kh[i >> 3][i & 7] = a;
-      kl[i >> 3][i & 7] = c;
-      split_f16(vreg[i >> 2][i & 3] * kQKScale, a, c);
-      vh[i >> 3][i & 7] = a;
-      vl[i >> 3][i & 7] = c;
+    for (int i = 0; i < EPT; i += 2) {
+      ea_half2 h2, l2;
+      split2(kreg[i >> 2][i & 3] * kQKScale, kreg[i >> 2][(i & 3) + 1] * kQKScale, h2, l2);
+      kh[i >> 3][i & 7] = h2[0];
+      kh[i >> 3][(i & 7) + 1] = h2[1];
+      kl[i >> 3][i & 7] = l2[0];
+      kl[i >> 3][(i & 7) + 1] = l2[1];
+      split2(vreg[i >> 2][i & 3] * kQKScale, vreg[i >> 2][(i & 3) + 1] * kQKScale, h2, l2);
+      vh[i >> 3][i & 7] = h2[0];
+      vh[i >> 3][(i & 7) + 1] = h2[1];
+      vl[i >> 3][i & 7] = l2[0];
+      vl[i >> 3][(i & 7) + 1] = l2[1];
     }
 #pragma unroll
     for (int u = 0; u < EPT / 8; ++u) {
@@ -175,12 +202,13 @@ __global__ __launch_bounds__(64 * NW) void encoder_attention_f16_kernel(const fl
   const int trow = 4 * (g >> 1) + (gi >> 2), tcol = 16 * (g & 1) + 4 * (gi & 3);
   const int ntile = (T + kEaKeys - 1) / kEaKeys;
   fetch(0);
+  stage(0);
+  __syncthreads();
+  if (ntile > 1) fetch(kEaKeys);  // tile 1 in flight during tile 0
   for (int kt = 0; kt < ntile; ++kt) {
     const int key0 = kt * kEaKeys;
-    __syncthreads();  // previous tile's readers are done
-    stage();
-    __syncthreads();
-    if (kt + 1 < ntile) fetch(key0 + kEaKeys);  // next tile in flight during this one
+    const _Float16(*kls)[kEaKeys * kEaLd] = klsb[kt & 1];
+    const _Float16(*vls)[kEaKeys * kEaLd] = vlsb[kt & 1];
 #pragma unroll
     for (int sub = 0; sub < kEaKeys / 32; ++sub) {
       floatx16 st;
@@ -198,43 +226,59 @@ __global__ __launch_bounds__(64 * NW) void encoder_attention_f16_kernel(const fl
         }
       }
       // online softmax of query l32 over these 32 keys (16 here, 16 in lane ^ 32)
+      if (key0 + sub * 32 + 32 > T) {  // only the last tile holds keys past T (wave-uniform)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = key0 + sub * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+          if (key >= T) st[i] = -INFINITY;
+        }
+      }
       float mx = -INFINITY;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = key0 + sub * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
-        if (key >= T) st[i] = -INFINITY;
-        mx = fmaxf(mx, st[i]);
-      }
+      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, st[i]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx);  // scores (and m) carry the 2^10 operand scale
-      const float alpha = __builtin_amdgcn_exp2f((m - mn) * kSInv);  // exp2(-inf) = 0
+      // lazy reference maximum (as the decoder cross-attention's softmax_entry):
+      // the running reference m only moves when the tile's maximum exceeds
+      // it by more than 1 (base 2), so p <= 2 and most tiles need no rescale
+      // of o (alpha == 1 exactly, skipped when the whole wave agrees); any
+      // reference gives the same softmax.  Scores (and m) carry the 2^10
+      // operand scale.
+      float mn = fmaxf(m, mx);
+      if (m != -INFINITY && mn - m <= kEaLazyMax) mn = m;
+      const float alpha = __builtin_amdgcn_exp2f((m - mn) * kSInv);  // exp2(-inf) = 0; 1 when mn == m
       float rs = 0.0f;
+      // mn is finite: the first 32 keys of tile 0 hold key 0 (< T)
+      const float nmn = -mn * kSInv;  // exact (power-of-two scale)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        st[i] = __builtin_amdgcn_exp2f((st[i] - mn) * kSInv);
+        st[i] = __builtin_amdgcn_exp2f(fmaf(st[i], kSInv, nmn));
         rs += st[i];
       }
       rs += __shfl_xor(rs, 32, 64);
       l = l * alpha + rs;
       m = mn;
+      if (__builtin_amdgcn_ballot_w64(alpha != 1.0f) != 0) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        o[0][i] *= alpha;
-        o[1][i] *= alpha;
+        for (int i = 0; i < 16; ++i) {
+          o[0][i] *= alpha;
+          o[1][i] *= alpha;
+        }
       }
       // P^T operands: MFMA t takes accumulator registers 8 t .. 8 t + 7.
-      // p in (0, 1] is split at p * 2^15 (exact scaling; undone at the end)
+      // p in (0, 2] is split at p * 2^14 (exact scaling; undone at the end)
       // so that the lo part of a small p stays a normal f16: 22 bits for
-      // every p >= 2^-18 instead of an absolute 2^-24 floor
+      // every p >= 2^-17 instead of an absolute 2^-24 floor
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         half8 ph, pl;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          _Float16 a, c;
-          split_f16(st[8 * t + j] * kPScale, a, c);
-          ph[j] = a;
-          pl[j] = c;
+        for (int j = 0; j < 8; j += 2) {
+          ea_half2 h2, l2;
+          split2(st[8 * t + j] * kPScale, st[8 * t + j + 1] * kPScale, h2, l2);
+          ph[j] = h2[0];
+          ph[j + 1] = h2[1];
+          pl[j] = l2[0];
+          pl[j + 1] = l2[1];
         }
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
@@ -254,6 +298,14 @@ __global__ __launch_bounds__(64 * NW) void encoder_attention_f16_kernel(const fl
         }
       }
     }
+    // the next tile into the other buffer (its last readers, tile kt - 1,
+    // passed the barrier below one iteration ago), then the one after it
+    // into registers
+    if (kt + 1 < ntile) {
+      stage((kt + 1) & 1);
+      if (kt + 2 < ntile) fetch(key0 + 2 * kEaKeys);
+    }
+    __syncthreads();
   }
   if (q < T) {
     const int row = b * T + q;
