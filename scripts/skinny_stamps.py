@@ -1,5 +1,8 @@
 """Phase timing of the decode-step GEMM from its in-kernel stamps (WQ4_STAMP
-build: make -C whisper-burn_amd stamp; run with WQ4_LIB_DIR=.../diag/stamp).
+build: make -C whisper-burn_amd stamp; run with WQ4_LIB_DIR=.../diag/stamp),
+or, with GETTER=decode, of the 8-wave decode kernel the model runs by
+default (make -C whisper-burn_amd variant V=stamp DEFS=-DWQ4_STAMP=1,
+WQ4_LIB_DIR=.../diag/stamp).
 
 Decodes one group of 32 Large-V3 clips for a few steps, then, per GEMM shape
 (N, K), averages over the graph-replayed launches of the last step:
@@ -25,11 +28,13 @@ mel = torch.from_numpy(np.stack([whisper_amd.synth_uniform(0x5EED0000 + c, "mel"
 m.transcribe(mel, 50259, 8, eot_stop=False)
 torch.cuda.synchronize()
 L = wq4.lib()
-L.wq4_diag_skinny_stamps.restype = ctypes.c_int
-NL, NW, NS = 512, 512, 8
+DECODE = os.environ.get("GETTER") == "decode"
+get = L.wq4_diag_decode_stamps if DECODE else L.wq4_diag_skinny_stamps
+get.restype = ctypes.c_int
+NL, NW, NS = 512, (256 if DECODE else 512), 8
 buf = np.zeros(NL * NW * NS, np.uint64)
 meta = np.zeros(NL * 3, np.int32)
-n = L.wq4_diag_skinny_stamps(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)),
+n = get(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)),
                              meta.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), NL)
 print("stamped launches", n)
 buf = buf.reshape(NL, NW, NS).astype(np.int64)

@@ -46,6 +46,8 @@ struct EpiArgs {
   // activation range); nullptr = the fixed kActScale of every internal
   // producer (wq4_device.hpp split_act).
   const float* act_inv;
+  // timing diagnostics (WQ4_STAMP builds only): the decode kernel's launch slot
+  int stamp_id;
 };
 
 // Output element index.  Row-major by default; head-major (hm_t > 0) writes

@@ -475,10 +475,37 @@ __device__ __forceinline__ void decode_epilogue(const floatx16& s, float cs, int
 __host__ __device__ constexpr size_t decode_lds_bytes_dev(int w) {
   return (size_t)(w == 8 ? w : w - 1) * 16 * 64 * 4 + (size_t)32 * kStageLd * 4;
 }
+// + LNA row stats, + LayerNorm-fold mean / den [32] each and the producer's x stage [32][33]
+__host__ __device__ constexpr size_t decode_lds_bytes_all(int w) {
+  return decode_lds_bytes_dev(w) + 2 * 64 * 4 + (64 + 32 * 33) * 4;
+}
+
 
 #ifndef WQ4_DIAG
 #define WQ4_DIAG 0
 #endif
+// WQ4_STAMP (timing diagnostics only: make variant V=stamp DEFS=-DWQ4_STAMP=1,
+// scripts/skinny_stamps.py with GETTER=decode; 0 in the product): the 8-wave
+// plans record per launch and workgroup s_memrealtime at the start, after
+// every operand load landed, after the MFMA loop, after the reduction
+// barrier and at the end of the epilogue, plus s_memtime cycles.
+#ifndef WQ4_STAMP
+#define WQ4_STAMP 0
+#endif
+constexpr int kDStampLaunches = 512, kDStampWgs = 256, kDStampSlots = 8;
+#if WQ4_STAMP
+__device__ unsigned long long g_dec_stamps[kDStampLaunches * kDStampWgs * kDStampSlots];
+#endif
+__device__ __forceinline__ unsigned long long dstamp_rt() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+__device__ __forceinline__ unsigned long long dstamp_cyc() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
 // Q4_0 weights at f16x2: block-scaled products (1, the product) -- per Q4
 // block t = MFMA(x_hi, q0) + MFMA(x_lo, q0) + MFMA(x_hi, q1) + MFMA(x_lo, q1)
 // (q - 8 exact in f16, f32 accumulation), then acc = fma(t, d', acc) for the
@@ -499,6 +526,11 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int mtiles = MT;
   constexpr int kRedWaves = W == 8 ? W : W - 1;
+  unsigned long long st_[kDStampSlots] = {};
+  if constexpr (WQ4_STAMP && W == 8) {
+    st_[0] = dstamp_rt();
+    st_[5] = dstamp_cyc();
+  }
   float* red = reinterpret_cast<float*>(smem);                          // [kRedWaves][16][64]
   float* stage = reinterpret_cast<float*>(smem) + kRedWaves * 16 * 64;  // [32][kStageLd]
 
@@ -693,6 +725,10 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
     }
   }
 
+  if constexpr (WQ4_STAMP && W == 8) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_[1] = dstamp_rt();
+  }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     floatx16 acc0, acc1;
@@ -765,18 +801,24 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
       // whole K in this workgroup: every wave finalises 2 of the 16
       // accumulator registers (same wave-order sum as the 4-wave path) and
       // applies their epilogue -- the reduction and epilogue run 8-wide
+      if constexpr (WQ4_STAMP) st_[2] = dstamp_rt();
 #pragma unroll
-      for (int i = 0; i < 16; ++i) red[(wave * 16 + i) * 64 + lane] = acc[i];
+      for (int i = 0; i < 16; ++i)
+        if (i < jmax) red[(wave * 16 + i) * 64 + lane] = acc[i];  // registers of real rows only
       __syncthreads();
+      if constexpr (WQ4_STAMP) st_[3] = dstamp_rt();
       const int h = lane >> 5;
       const int col = nt * 32 + r;
       float v[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int i = 2 * wave + q;
-        v[q] = red[i * 64 + lane];
+        v[q] = 0.0f;  // rows past M: 0 (never stored)
+        if (i < jmax) {
+          v[q] = red[i * 64 + lane];
 #pragma unroll
-        for (int w = 1; w < W; ++w) v[q] = v[q] + red[(w * 16 + i) * 64 + lane];
+          for (int w = 1; w < W; ++w) v[q] = v[q] + red[(w * 16 + i) * 64 + lane];
+        }
       }
       typedef __attribute__((address_space(1))) int gint;
       gint* ctr = (gint*)(counters + nt);
@@ -862,6 +904,16 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
         }
       }
       if (ks > 1 && tid == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+#if WQ4_STAMP
+      if (tid == 0 && e.stamp_id >= 0 && e.stamp_id < kDStampLaunches && blockIdx.x < kDStampWgs) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st_[4] = dstamp_rt();
+        st_[6] = dstamp_cyc();
+        st_[7] = (unsigned long long)cnt;
+        for (int q = 0; q < kDStampSlots; ++q)
+          g_dec_stamps[((size_t)e.stamp_id * kDStampWgs + blockIdx.x) * kDStampSlots + q] = st_[q];
+      }
+#endif
       continue;  // MT == 1 for 8-wave plans
     }
 
@@ -947,8 +999,9 @@ static size_t prefill_lds_bytes(int ns, int epi) {
   return a > s ? a : s;
 }
 
-// + LNA row stats, + LayerNorm-fold mean / den [32] each and the producer's x stage [32][33]
-static size_t decode_lds_bytes(int w) { return decode_lds_bytes_dev(w) + 2 * 64 * 4 + (64 + 32 * 33) * 4; }
+static size_t decode_lds_bytes(int w) { return decode_lds_bytes_all(w); }
+
+
 
 DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal) {
   // Smallest per-wave depth whose grid still covers ~all CUs, then balance.
@@ -1064,6 +1117,10 @@ hipError_t launch_tile_activations(const float* x, _Float16* at, int M, int K, i
   return hipGetLastError();
 }
 
+// Stamp bookkeeping (WQ4_STAMP builds): launch slot -> (N, K, rows).
+static int g_dstamp_next = 0;
+static int g_dstamp_meta[kDStampLaunches][3];
+
 template <int NS, int EPI, int WK>
 static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* cs,
                                 const _Float16* at, int rows, const EpiArgs& e, const DecodeWs* ws,
@@ -1088,9 +1145,17 @@ static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint3
   }
   if (dec_ok) {
     const dim3 grid((unsigned)(g.ntiles * p.ks));
+    EpiArgs es = e;
+    es.stamp_id = -1;
+    if (WQ4_STAMP && p.w == 8 && g_dstamp_next < kDStampLaunches) {
+      es.stamp_id = g_dstamp_next++;
+      g_dstamp_meta[es.stamp_id][0] = (int)g.n;
+      g_dstamp_meta[es.stamp_id][1] = (int)g.k;
+      g_dstamp_meta[es.stamp_id][2] = rows;
+    }
 #define WQ4_DEC(PER_, MT_, W_)                                                                               \
   hipLaunchKernelGGL((q4_gemm_decode_kernel<NS, EPI, PER_, MT_, W_, WK>), grid, dim3(64 * W_), decode_lds_bytes(W_), \
-                     st, nib, sc, cs, at, mt0, (int)g.nbp, p.ks, p.chunk, ws->part, ws->counters, e)
+                     st, nib, sc, cs, at, mt0, (int)g.nbp, p.ks, p.chunk, ws->part, ws->counters, es)
     // 8-wave plans: one m-tile per launch (two would not fit the registers);
     // 4-wave plans: m-tiles in launches of <= 2.  Launches on one stream
     // complete in order, so they share the workspace and counters.
@@ -1150,3 +1215,23 @@ hipError_t launch_q4_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* s
 }
 
 }  // namespace wq4
+
+// Timing diagnostics (WQ4_STAMP builds only; returns 0 launches otherwise):
+// copies [launches][kDStampWgs][8] stamps of the 8-wave decode kernel and
+// [launches][3] (N, K, rows).
+extern "C" int wq4_diag_decode_stamps(unsigned long long* out, int* meta, int max_launches) {
+#if WQ4_STAMP
+  const int n = wq4::g_dstamp_next < max_launches ? wq4::g_dstamp_next : max_launches;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(wq4::g_dec_stamps),
+                          (size_t)n * wq4::kDStampWgs * wq4::kDStampSlots * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < 3; ++j) meta[i * 3 + j] = wq4::g_dstamp_meta[i][j];
+  return n;
+#else
+  (void)out;
+  (void)meta;
+  (void)max_launches;
+  return 0;
+#endif
+}

@@ -225,31 +225,50 @@ __global__ __launch_bounds__(64 * kSkW) void skinny_gemm_kernel(const uint32_t* 
   // epilogue operands of this thread's outputs (row o / COLS, column o %
   // COLS, o = tid + 512 j), loaded up front (never written by this launch
   // before its own epilogue)
+  // All of them branch-free buffer loads (an absent operand is a zero-size
+  // resource, an element out of range an out-of-range offset: both read 0):
+  // a load under an exec branch makes the compiler drain vmcnt at the join,
+  // a whole memory round trip before the weight stream is issued (the
+  // 8-wave decode kernel's finding, tools/warm_cold.py; here the stamped
+  // operand phase fell from 3.3-4.0 us to ~2.3 at one clip).
   constexpr int OPT = (OUT + 511) / 512;
   float pre_bias[OPT], pre_res[OPT], pre_wg[OPT], pre_g[OPT];
+  {
+    const uint32_t nb = (uint32_t)e.n * 4;
+    const __amdgpu_buffer_rsrc_t rbias = rsrc(e.bias, e.bias ? nb : 0);
+    const __amdgpu_buffer_rsrc_t rwg = rsrc(e.lnf_wg, e.lnf_stats_in ? nb : 0);
+    const __amdgpu_buffer_rsrc_t rg = rsrc(e.lnf_g, e.lnf_at ? nb : 0);
+    const __amdgpu_buffer_rsrc_t rres = rsrc(e.residual, e.residual ? (uint32_t)e.m * (uint32_t)e.ldo * 4u : 0);
 #pragma unroll
-  for (int j = 0; j < OPT; ++j) {
-    const int o = tid + 512 * j, orow = r0 + o / COLS, n = nt * COLS + o % COLS;
-    const bool ok = o < OUT && orow < e.m && n < e.n;
-    pre_bias[j] = ok && e.bias ? e.bias[n] : 0.0f;
-    pre_res[j] = ok && e.residual ? e.residual[(size_t)orow * e.ldo + n] : 0.0f;
-    pre_wg[j] = ok && e.lnf_stats_in ? e.lnf_wg[n] : 0.0f;
-    pre_g[j] = ok && e.lnf_at ? e.lnf_g[n] : 0.0f;
+    for (int j = 0; j < OPT; ++j) {
+      const int o = tid + 512 * j, orow = r0 + o / COLS, n = nt * COLS + o % COLS;
+      const bool ok = o < OUT && orow < e.m && n < e.n;
+      const int coff = ok ? n * 4 : kOobS;
+      pre_bias[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbias, coff, 0, 0));
+      pre_wg[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rwg, coff, 0, 0));
+      pre_g[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, coff, 0, 0));
+      pre_res[j] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rres, ok ? (orow * e.ldo + n) * 4 : kOobS, 0, 0));
+    }
   }
   const float ainv = (e.act_inv ? *e.act_inv : kActScaleInv) * binv;
   // LayerNorm fold, consumer: thread (row tid / 16, part tid % 16) loads the
   // row's 16-column tile statistics j = part, part + 16, ... first
   floatx2 lnf_st[kSkLnPer];
   const int lrow = r0 + (tid >> 4), lpart = tid & 15;  // threads tid < 256: this tile's 16 rows
-  if (e.lnf_stats_in) {
+  {
+    const __amdgpu_buffer_rsrc_t rst =
+        rsrc(e.lnf_stats_in, e.lnf_stats_in ? (uint32_t)e.m * (uint32_t)e.lnf_tiles * 8u : 0);
 #pragma unroll
     for (int v = 0; v < kSkLnPer; ++v) {
       const int j = lpart + 16 * v;
-      lnf_st[v] = (tid < 256 && lrow < e.m && j < e.lnf_tiles)
-                      ? *reinterpret_cast<const floatx2*>(e.lnf_stats_in + ((size_t)lrow * e.lnf_tiles + j) * 2)
-                      : floatx2{0.0f, 0.0f};
+      lnf_st[v] = __builtin_bit_cast(
+          floatx2, __builtin_amdgcn_raw_buffer_load_b64(
+                       rst, (tid < 256 && lrow < e.m && j < e.lnf_tiles) ? (lrow * e.lnf_tiles + j) * 8 : kOobS, 0, 0));
     }
   }
+  // keep every epilogue-operand / statistics load above the weight stream
+  __builtin_amdgcn_sched_barrier(0);
 
   const int nt16 = nt * NT;
   const __amdgpu_buffer_rsrc_t rw =
