@@ -382,6 +382,43 @@ def test_gemm_headmajor_layout(torch, policy):
                                              ctypes.c_void_p(hm.data_ptr()), m, 25, d, wq4.PREC_F16X2, policy, st))
 
 
+@pytest.mark.parametrize("clips", [1, 2])
+def test_gemm_headmajor_ring_kernel(torch, clips):
+    """The few-clip cross K / V cache GEMMs (wa_model.cpp cross_kv_forward:
+    M = clips x 1500 rows, head-major output) run on the encoder ring kernel
+    (wq4_enc.hip); their bits equal the prefill tile kernel's row-major
+    result permuted to [g][head][t][64]."""
+    import ctypes
+
+    d = k = 1280
+    trows, m = 1500, 1500 * clips
+    rng = np.random.default_rng(1500 + clips)
+    q = oracle.quantize_convert_np((rng.standard_normal(d * k) * 0.05).astype(np.float32))
+    t = wq4.Q4Tensor.from_q4_bytes(q, [d, k], decode_step=False)
+    x = to_dev(torch, rng.standard_normal(m * k).astype(np.float32), (m, k))
+    b = to_dev(torch, (rng.standard_normal(d) * 0.1).astype(np.float32), (d,))
+    L = wq4.lib()
+    atb = L.wq4_atiled_bytes(m, k, wq4.PREC_F16X2)
+    at = torch.zeros(atb, dtype=torch.uint8, device="cuda:0")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    wq4.check(L.wq4_tile_activations(ctypes.c_void_p(x.data_ptr()), m, k, k, wq4.PREC_F16X2,
+                                     ctypes.c_void_p(at.data_ptr()), atb, st))
+    ref = torch.empty((m, d), device="cuda:0", dtype=torch.float32)
+    hm = torch.empty((m * d,), device="cuda:0", dtype=torch.float32)
+    prev = L.wq4_debug_set_enc_kernel(0)  # the tile kernel for the row-major reference
+    try:
+        wq4.check(L.wq4_gemm_tiled(t.handle, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(at.data_ptr()), None,
+                                   ctypes.c_void_p(ref.data_ptr()), None, m, 0, wq4.PREC_F16X2, 1, st))
+        assert L.wq4_debug_set_enc_kernel(1) >= 0  # by rows: the ring kernel at these grids
+        wq4.check(L.wq4_gemm_tiled_headmajor(t.handle, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(at.data_ptr()),
+                                             ctypes.c_void_p(hm.data_ptr()), m, trows, d, wq4.PREC_F16X2, 0, st))
+        torch.cuda.synchronize()
+    finally:
+        L.wq4_debug_set_enc_kernel(prev)
+    want = ref.cpu().numpy().reshape(clips, trows, d // 64, 64).transpose(0, 2, 1, 3).ravel()
+    assert np.array_equal(hm.cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("wtype", ["q4_0", "f16"])
 @pytest.mark.parametrize("prec", [0, 1])
 @pytest.mark.parametrize("m,n,flags", [(1, 3840, 0), (17, 1280, 0), (32, 5120, 5), (100, 1280, 2), (128, 96, 0)])

@@ -301,7 +301,7 @@ __global__ __launch_bounds__(64 * WM * 4, WM == 2 ? 2 : 3) void q4_gemm_enc_kern
 #pragma unroll
   for (int nt = 0; nt < TN; ++nt) cs[nt] = nt0 + nt < ntiles ? colscale[(nt0 + nt) * 32 + r] * ainv : 1.0f;
 
-  if constexpr (EPI == kEpiF32) {
+  if constexpr (EPI == kEpiF32 || EPI == kEpiHeadMajor) {
 #pragma unroll
     for (int mt = 0; mt < TM; ++mt)
 #pragma unroll
@@ -310,10 +310,12 @@ __global__ __launch_bounds__(64 * WM * 4, WM == 2 ? 2 : 3) void q4_gemm_enc_kern
         for (int i = 0; i < 16; ++i) {
           const int row = (mt0 + mt) * 32 + acc_row_e(i, h);
           const int col = (nt0 + nt) * 32 + r;
-          if (row < e.m && col < e.n) e.out[(size_t)row * e.ldo + col] = epi_value(acc[mt][nt][i] * cs[nt], row, col, e);
+          if (row < e.m && col < e.n)
+            e.out[EPI == kEpiHeadMajor ? out_index(e, row, col) : (size_t)row * e.ldo + col] =
+                epi_value(acc[mt][nt][i] * cs[nt], row, col, e);
         }
   } else {
-    static_assert(EPI == kEpiTiled, "f32 or A-tiled outputs");
+    static_assert(EPI == kEpiTiled, "f32, head-major f32 or A-tiled outputs");
     float* stage = reinterpret_cast<float*>(smem) + wave * (32 * kStageLdE);
     const size_t kbp_next = (size_t)e.nbp_next * 2;
     half8* dst = reinterpret_cast<half8*>(e.out_tiled);
@@ -388,7 +390,7 @@ static std::atomic<int> g_enc_mode{[] {
 // < 400 workgroups, the tile kernel above.
 int enc_gemm_pick(const Q4Geom& g, int rows, int epi_mode, int ns, int wtype) {
   const int mode = g_enc_mode.load();
-  if (mode == 0 || ns != 2 || wtype != kWeightsQ4 || (epi_mode != kEpiF32 && epi_mode != kEpiTiled) || rows <= 128 ||
+  if (mode == 0 || ns != 2 || wtype != kWeightsQ4 || rows <= 128 ||
       g.kb < 1)
     return 0;
   if (mode >= 2) return mode;
@@ -409,6 +411,9 @@ static hipError_t launch_enc_t(const Q4Geom& g, const uint8_t* nib, const uint32
   if (epi_mode == kEpiTiled)
     hipLaunchKernelGGL((q4_gemm_enc_kernel<WM, TM, TN, kEpiTiled>), grid, dim3(G::THREADS), lds, st, nib, sc, cs, at,
                        mtiles, (int)g.nbp, (int)g.ntiles, e);
+  else if (epi_mode == kEpiHeadMajor)  // the cross K / V cache GEMMs (wq4_gemm_tiled_headmajor)
+    hipLaunchKernelGGL((q4_gemm_enc_kernel<WM, TM, TN, kEpiHeadMajor>), grid, dim3(G::THREADS), lds, st, nib, sc, cs,
+                       at, mtiles, (int)g.nbp, (int)g.ntiles, e);
   else
     hipLaunchKernelGGL((q4_gemm_enc_kernel<WM, TM, TN, kEpiF32>), grid, dim3(G::THREADS), lds, st, nib, sc, cs, at,
                        mtiles, (int)g.nbp, (int)g.ntiles, e);
