@@ -36,7 +36,7 @@ def _sdpa64(q, k, v, causal_from=None):
     return p @ v.astype(np.float64)
 
 
-@pytest.mark.parametrize("H,B", [(20, 1), (16, 2)])
+@pytest.mark.parametrize("H,B", [(20, 1), (16, 2), (20, 3)])  # 4-wave (few clips) and 8-wave workgroups
 def test_encoder_attention_whisper_size(H, B):
     import torch
 

@@ -324,7 +324,19 @@ __global__ __launch_bounds__(64 * NW, WA_EA_WAVES) void encoder_attention_f16_ke
 
 hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Float16* tiled, int ns,
                                     hipStream_t st) {
-  const dim3 g2((T + 255) / 256, H, B);  // 8 waves x 32 queries
+  // 8 waves x 32 queries per workgroup; when that grid leaves most CUs idle
+  // (one or two clips: 120 / 240 workgroups at Large-V3) 4 waves, twice the
+  // workgroups (each query's arithmetic is the same either way)
+  const bool few = (int64_t)B * H * ((T + 255) / 256) < 256;
+  if (few) {
+    const dim3 g4((T + 127) / 128, H, B);
+    if (ns == 2)
+      hipLaunchKernelGGL((encoder_attention_f16_kernel<2, 4>), g4, dim3(256), 0, st, qkv, T, H, tiled);
+    else
+      hipLaunchKernelGGL((encoder_attention_f16_kernel<1, 4>), g4, dim3(256), 0, st, qkv, T, H, tiled);
+    return hipGetLastError();
+  }
+  const dim3 g2((T + 255) / 256, H, B);
   if (ns == 2)
     hipLaunchKernelGGL((encoder_attention_f16_kernel<2, 8>), g2, dim3(512), 0, st, qkv, T, H, tiled);
   else
