@@ -135,3 +135,36 @@ def test_xattn_rows_independent(torch):
     full = whisper_amd.xattn_check(q, rk, rk, bv, enc, 1, H)
     one = whisper_amd.xattn_check(q[2:3], rk, rk, bv, enc[2:3], 1, H)
     assert torch.equal(full[2:3], one)
+
+
+@pytest.mark.parametrize("B,Tq,T,H", [
+    (1, 1, 1500, 20),   # Large-V3, one clip (BASELINE config 3): the product's few-clip form
+    (3, 1, 1500, 20),
+    (1, 4, 1500, 20),   # one clip's prompt rows
+    (8, 1, 1500, 16),   # Medium, the largest few-clip group
+    (2, 3, 37, 6),      # short T (one split), the auto-language prompt's 3 rows
+    (5, 1, 200, 6),
+])
+def test_xattn_kv_cache_form(torch, B, Tq, T, H):
+    """The few-clip cross-attention over cached K / V (cross_attn_kv_kernel,
+    attention.rs:177-236's cached form: f32 products, online softmax, split
+    merge by the last arriver) against float64 softmax(q K^T / 8) V."""
+    import whisper_amd
+
+    rng = np.random.default_rng(B * 100 + Tq * 10 + H)
+    D = 64 * H
+    q = (2.0 * rng.standard_normal((B * Tq, D))).astype(np.float32)
+    k = rng.standard_normal((B, H, T, 64)).astype(np.float32)
+    v = rng.standard_normal((B, H, T, 64)).astype(np.float32)
+    got = whisper_amd.xattn_kv_check(torch.from_numpy(q).cuda(), torch.from_numpy(k).cuda(),
+                                     torch.from_numpy(v).cuda(), Tq).cpu().numpy()
+    qh = q.astype(np.float64).reshape(B, Tq, H, 64)
+    s = np.einsum("bqhd,bhtd->bhqt", qh, k.astype(np.float64)) / 8.0
+    s -= s.max(axis=-1, keepdims=True)
+    p = np.exp(s)
+    p /= p.sum(axis=-1, keepdims=True)
+    ref = np.einsum("bhqt,bhtd->bqhd", p, v.astype(np.float64)).reshape(B * Tq, D)
+    # f32 products and sums over T keys, the output split into an exact-to-
+    # 2^-22 f16 pair (the output projection's operand) and read back
+    err = np.abs(got - ref).max() / np.abs(v).max()
+    assert err <= 2e-6, err

@@ -1511,6 +1511,26 @@ wq4_status wa_xattn_check(int device, const float* q_dev, const uint8_t* wk_dev,
   return WQ4_OK;
 }
 
+wq4_status wa_xattn_kv_check(int device, const float* q_dev, const float* k_dev, const float* v_dev, int n_clips,
+                             int Tq, int T, int H, wq4_precision prec, float* out_dev) {
+  if (!q_dev || !k_dev || !v_dev || !out_dev) return fail(WQ4_EINVAL, "null argument");
+  if (n_clips < 1 || Tq < 1 || Tq > 4 || T < 1 || H < 1) return fail(WQ4_EINVAL, "bad sizes");
+  const int D = 64 * H, ns = prec == WQ4_PREC_F16 ? 1 : 2, R = n_clips * Tq;
+  WA_HIP(hipSetDevice(device));
+  Dev d;
+  auto* part = d.alloc<float>(wa::cross_attention_kv_part_floats(n_clips, H, T));
+  auto* ctr = d.alloc<int>((size_t)n_clips * H);
+  const size_t tb = wq4_atiled_bytes(R, D, prec);
+  auto* tiled = d.alloc<_Float16>(tb / 2);
+  if (!part || !ctr || !tiled) return fail(WQ4_ENOMEM, "allocation failed");
+  WA_HIP(hipMemset(ctr, 0, (size_t)n_clips * H * sizeof(int)));
+  WA_HIP(hipMemset(tiled, 0, tb));
+  WA_HIP(wa::launch_cross_attention_kv(q_dev, k_dev, v_dev, n_clips, Tq, T, H, part, ctr, tiled, ns, nullptr));
+  WA_HIP(wa::launch_untile(tiled, R, D, ns, out_dev, nullptr));
+  WA_HIP(hipDeviceSynchronize());
+  return WQ4_OK;
+}
+
 wq4_status wa_encoder_attention_check(int device, const float* qkv_dev, int n_clips, int T, int H, wq4_precision prec,
                                       float* out_dev) {
   if (!qkv_dev || !out_dev) return fail(WQ4_EINVAL, "null argument");

@@ -68,11 +68,12 @@ def lib() -> ctypes.CDLL:
         L.wa_log_mel.argtypes = [c_int, vp, c_int, c_i64, c_i64, c_int, vp, vp]
         L.wa_mel_filterbank.argtypes = [c_int, f32p, f32p]
         L.wa_xattn_check.argtypes = [c_int, vp, vp, vp, vp, c_int, vp, c_int, c_int, c_int, c_int, c_int, vp]
+        L.wa_xattn_kv_check.argtypes = [c_int, vp, vp, vp, c_int, c_int, c_int, c_int, c_int, vp]
         L.wa_transcribe_trace.argtypes = [vp, vp, c_int, c_int, c_int, c_int, i32p, i32p, vp, c_int, vp, vp]
         L.wa_encoder_attention_check.argtypes = [c_int, vp, c_int, c_int, c_int, c_int, vp]
         L.wa_self_attention_check.argtypes = [c_int, vp, vp, vp, c_int, c_int, c_int, c_int, c_int, c_int, vp]
         L.wa_logits_argmax_check.argtypes = [c_int, vp, vp, c_int, c_int, c_int, c_int, c_int, vp, vp]
-        for n in ("wa_xattn_check", "wa_transcribe_trace", "wa_encoder_attention_check", "wa_self_attention_check",
+        for n in ("wa_xattn_check", "wa_xattn_kv_check", "wa_transcribe_trace", "wa_encoder_attention_check", "wa_self_attention_check",
                   "wa_logits_argmax_check", "wa_log_mel", "wa_mel_filterbank", "wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
                   "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read", "wa_probe_kernels",
                   "wa_decode_group_rows",
@@ -151,6 +152,19 @@ def xattn_check(q, wk_raw, wv_raw, bv, enc, Tq: int, H: int, weight_type: int = 
     ptr = lambda t: ctypes.c_void_p(t.contiguous().data_ptr())
     check(lib().wa_xattn_check(dev, ptr(q), ptr(wk_raw), ptr(wv_raw), ptr(bv), weight_type, ptr(enc), B, Tq, T, H,
                                precision, ptr(out)))
+    return out
+
+
+def xattn_kv_check(q, k, v, Tq: int, precision: int = wq4.PREC_F16X2):
+    """The few-clip cross-attention over cached K / V (wa_xattn_kv_check):
+    q cuda f32 [B*Tq, 64H], k / v cuda f32 head-major [B, H, T, 64] ->
+    [B*Tq, 64H] (softmax(q K^T / 8) V per head)."""
+    torch = _torch()
+    B, H, T, _ = k.shape
+    out = torch.empty((B * Tq, 64 * H), device=k.device, dtype=torch.float32)
+    dev = k.device.index if k.device.index is not None else 0
+    ptr = lambda t: ctypes.c_void_p(t.contiguous().data_ptr())
+    check(lib().wa_xattn_kv_check(dev, ptr(q), ptr(k), ptr(v), B, Tq, T, H, precision, ptr(out)))
     return out
 
 
