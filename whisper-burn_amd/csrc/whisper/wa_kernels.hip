@@ -352,44 +352,64 @@ hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Floa
 
 // Online-softmax scan of keys [k0, k1).  rows(j, kp, vp) yields this lane's
 // 4-float K / V pointers of key j; vis(t, j) says whether query t sees key j.
-template <int TQ, int U, class Rows, class Vis>
-__device__ __forceinline__ void attn_scan(const floatx4 (&qv)[TQ], int Tq, int k0, int k1, int grp, Rows rows,
-                                          Vis vis, float (&m)[TQ], float (&l)[TQ], floatx4 (&o)[TQ]) {
+// attn_fetch issues one pass's loads (4 U keys per wave), attn_update folds
+// them in; attn_scan alternates the two.  A caller may issue the first pass's
+// loads itself before its queries exist (cross_attn_kv_kernel, FUSEQ).
+template <int TQ>
+__device__ __forceinline__ void attn_init(float (&m)[TQ], float (&l)[TQ], floatx4 (&o)[TQ]) {
 #pragma unroll
   for (int t = 0; t < TQ; ++t) {
     m[t] = -INFINITY;
     l[t] = 0.0f;
     o[t] = floatx4{0.f, 0.f, 0.f, 0.f};
   }
-  for (int j0 = k0; j0 < k1; j0 += 4 * U) {
-    floatx4 kk[U], vv[U];
+}
+
+template <int U, class Rows>
+__device__ __forceinline__ void attn_fetch(int j0, int k1, int grp, Rows rows, floatx4 (&kk)[U], floatx4 (&vv)[U]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = min(j0 + 4 * u + grp, k1 - 1);  // clamped: loads never branch
-      const float *kp, *vp;
-      rows(j, kp, vp);
-      kk[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(kp));
-      vv[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(vp));
-    }
+  for (int u = 0; u < U; ++u) {
+    const int j = max(0, min(j0 + 4 * u + grp, k1 - 1));  // clamped: loads never branch
+    const float *kp, *vp;
+    rows(j, kp, vp);
+    kk[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(kp));
+    vv[u] = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(vp));
+  }
+}
+
+template <int TQ, int U, class Vis>
+__device__ __forceinline__ void attn_update(const floatx4 (&qv)[TQ], int Tq, int j0, int k1, int grp, Vis vis,
+                                            const floatx4 (&kk)[U], const floatx4 (&vv)[U], float (&m)[TQ],
+                                            float (&l)[TQ], floatx4 (&o)[TQ]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = j0 + 4 * u + grp;
+  for (int u = 0; u < U; ++u) {
+    const int j = j0 + 4 * u + grp;
 #pragma unroll
-      for (int t = 0; t < TQ; ++t) {
-        if (t < Tq) {
-          const float dot =
-              wq4::sum16(qv[t][0] * kk[u][0] + qv[t][1] * kk[u][1] + qv[t][2] * kk[u][2] + qv[t][3] * kk[u][3]);
-          if (j < k1 && vis(t, j)) {
-            const float mn = fmaxf(m[t], dot);
-            const float alpha = __builtin_amdgcn_exp2f(m[t] - mn);  // base-2 units
-            const float p = __builtin_amdgcn_exp2f(dot - mn);
-            l[t] = l[t] * alpha + p;
-            o[t] = o[t] * alpha + vv[u] * p;
-            m[t] = mn;
-          }
+    for (int t = 0; t < TQ; ++t) {
+      if (t < Tq) {
+        const float dot =
+            wq4::sum16(qv[t][0] * kk[u][0] + qv[t][1] * kk[u][1] + qv[t][2] * kk[u][2] + qv[t][3] * kk[u][3]);
+        if (j < k1 && vis(t, j)) {
+          const float mn = fmaxf(m[t], dot);
+          const float alpha = __builtin_amdgcn_exp2f(m[t] - mn);  // base-2 units
+          const float p = __builtin_amdgcn_exp2f(dot - mn);
+          l[t] = l[t] * alpha + p;
+          o[t] = o[t] * alpha + vv[u] * p;
+          m[t] = mn;
         }
       }
     }
+  }
+}
+
+template <int TQ, int U, class Rows, class Vis>
+__device__ __forceinline__ void attn_scan(const floatx4 (&qv)[TQ], int Tq, int k0, int k1, int grp, Rows rows,
+                                          Vis vis, float (&m)[TQ], float (&l)[TQ], floatx4 (&o)[TQ]) {
+  attn_init<TQ>(m, l, o);
+  for (int j0 = k0; j0 < k1; j0 += 4 * U) {
+    floatx4 kk[U], vv[U];
+    attn_fetch<U>(j0, k1, grp, rows, kk, vv);
+    attn_update<TQ, U>(qv, Tq, j0, k1, grp, vis, kk, vv, m, l, o);
   }
 }
 
@@ -442,6 +462,117 @@ __device__ __forceinline__ void attn_merge(int Tq, int wave, int lane, float (&m
   }
 }
 
+// ----------------------------- in-launch projections (few clips) --
+// A decode step of a few clips is a chain of launches; where an attention
+// workgroup owns whole heads it can form its own projection of them instead
+// of waiting for a GEMM launch: LN(x) of its clip's Tq rows (f32,
+// wq4_lnmath.hpp, layers.rs:12-32) and 64 output columns from the raw GGUF
+// Q4_0 rows (f32 dequantised weights, f32 sums: linear.rs:34-40 over
+// tensor.rs dequantisation).  Lane tid owns column tid >> 2 and block pairs
+// (tid & 3) + 4 i (36 B, dword aligned).
+constexpr int kXkvMaxD = 1280;  // LDS rows of LN(x); n_text_state <= 1280
+constexpr int kXkvPairs = 5;    // Q4 block pairs per lane: D / 64 / 4 <= 5
+
+// LN(x) of row r = wave into xs[wave] (f32), the wave's own rows only.
+template <int TQ>
+__device__ __forceinline__ void xkv_ln_rows(const float* x, const float* ln_w, const float* ln_b, int b, int Tq,
+                                            int D, int wave, int lane, float (*xs)[kXkvMaxD]) {
+  if (wave >= Tq) return;
+  const float* xr = x + (size_t)(b * Tq + wave) * D;
+  floatx4 v[wq4::kLnMaxV];
+#pragma unroll
+  for (int i = 0; i < wq4::kLnMaxV; ++i) {
+    const int k = lane * 4 + 256 * i;
+    v[i] = k < D ? *reinterpret_cast<const floatx4*>(xr + k) : floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  float mean, den;
+  wq4::ln_row_stats(v, D, lane, mean, den);
+#pragma unroll
+  for (int i = 0; i < wq4::kLnMaxV; ++i) {
+    const int k = lane * 4 + 256 * i;
+    if (k < D) {
+      const floatx4 g = *reinterpret_cast<const floatx4*>(ln_w + k);
+      const floatx4 bb = *reinterpret_cast<const floatx4*>(ln_b + k);
+      floatx4 y;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = wq4::ln_apply(v[i][e], mean, den, g[e], bb[e]);
+      *reinterpret_cast<floatx4*>(&xs[wave][k]) = y;
+    }
+  }
+}
+
+// This lane's words of 64 raw Q4_0 rows starting at w64 (K = D); past the
+// row: clamped address (the dot gives those pairs a zero weight).
+__device__ __forceinline__ void q4_rows_load(const uint8_t* w64, int D, int tid, uint32_t (&w)[kXkvPairs][9]) {
+  const int c = tid >> 2, jp = tid & 3, npairs = D / 64;
+  const uint32_t* wrow = reinterpret_cast<const uint32_t*>(w64 + (size_t)c * (D / 32) * 18);
+#pragma unroll
+  for (int i = 0; i < kXkvPairs; ++i) {
+    const int p = min(jp + 4 * i, npairs - 1);
+#pragma unroll
+    for (int e = 0; e < 9; ++e) w[i][e] = __builtin_nontemporal_load(wrow + p * 9 + e);
+  }
+}
+
+// One Q4_0 block (16 nibble bytes in n[4], scale d) dotted with LN(x)[k0 ..
+// k0 + 31] of every query row: element i = low nibble of byte i, i + 16 = high.
+template <int TQ>
+__device__ __forceinline__ void xkv_block_dot(const uint32_t (&n)[4], float d, int k0, int Tq,
+                                              const float (*xs)[kXkvMaxD], float (&acc)[TQ]) {
+#pragma unroll
+  for (int t = 0; t < TQ; ++t) {
+    if (t < Tq) {
+      float s = acc[t];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const floatx4 xl = *reinterpret_cast<const floatx4*>(&xs[t][k0 + 4 * w]);
+        const floatx4 xh = *reinterpret_cast<const floatx4*>(&xs[t][k0 + 16 + 4 * w]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t byte = (n[w] >> (8 * e)) & 0xffu;
+          s = fmaf(d * (float)((int)(byte & 15u) - 8), xl[e], s);
+          s = fmaf(d * (float)((int)(byte >> 4) - 8), xh[e], s);
+        }
+      }
+      acc[t] = s;
+    }
+  }
+}
+
+// Column (tid >> 2) of the 64 rows loaded by q4_rows_load, dotted with the
+// Tq rows of xs; every lane of the column's 4 returns the same sum (fixed
+// order: block pairs in order per lane, then lanes (0 + 1) + (2 + 3)).
+template <int TQ>
+__device__ __forceinline__ void q4_rows_dot(const uint32_t (&w)[kXkvPairs][9], int D, int tid, int Tq,
+                                            const float (*xs)[kXkvMaxD], float (&acc)[TQ]) {
+  const int jp = tid & 3, npairs = D / 64;
+#pragma unroll
+  for (int t = 0; t < TQ; ++t) acc[t] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < kXkvPairs; ++i) {
+    const bool ok = jp + 4 * i < npairs;
+    const int kp0 = (jp + 4 * i) * 64;
+    // block 2p: scale = bytes 0-1, nibbles = bytes 2-17; block 2p + 1:
+    // scale = bytes 18-19, nibbles = bytes 20-35 (words 5-8)
+    const float d0 = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[i][0] & 0xffffu));
+    const float d1 = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[i][4] >> 16));
+    const uint32_t n0[4] = {__builtin_amdgcn_alignbit(w[i][1], w[i][0], 16),
+                            __builtin_amdgcn_alignbit(w[i][2], w[i][1], 16),
+                            __builtin_amdgcn_alignbit(w[i][3], w[i][2], 16),
+                            __builtin_amdgcn_alignbit(w[i][4], w[i][3], 16)};
+    const uint32_t n1[4] = {w[i][5], w[i][6], w[i][7], w[i][8]};
+    if (ok) {
+      xkv_block_dot<TQ>(n0, d0, kp0, Tq, xs, acc);
+      xkv_block_dot<TQ>(n1, d1, kp0 + 32, Tq, xs, acc);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TQ; ++t) {
+    acc[t] += __shfl_xor(acc[t], 1, 64);
+    acc[t] += __shfl_xor(acc[t], 2, 64);
+  }
+}
+
 // ------------------------------------------ decoder self-attention --
 // One workgroup per (head, clip); the 4 waves split the keys 0 .. kv_len +
 // Tq - 1 (causal inside the new tokens).  Self-K/V caches are head-major
@@ -449,11 +580,16 @@ __device__ __forceinline__ void attn_merge(int Tq, int wave, int lane, float (&m
 // appended there for later steps and read here straight from the qkv rows.
 constexpr int kMaxCtx = 448;
 
-template <int NS, int TQ>
+// FUSE (few clips, Q4_0 weights): the workgroup forms its head's q, k, v
+// itself -- LN(x) of its clip's rows (attn_ln) and 3 x 64 columns of the raw
+// query / key / value rows (q4_rows_load / q4_rows_dot) -- instead of reading
+// the qkv GEMM's rows: one launch fewer per layer.  The new keys / values go
+// to the cache first and are read back from it after the barrier.
+template <int NS, int TQ, bool FUSE>
 __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restrict__ qkv, float* __restrict__ ck,
                                                             float* __restrict__ cv, int Tq_, int H, int ctx,
                                                             const DecodeState* state, int kv_len_host,
-                                                            _Float16* __restrict__ tiled) {
+                                                            _Float16* __restrict__ tiled, SelfFuseQkv fz) {
   const int Tq = TQ == 1 ? 1 : Tq_;
   __shared__ float wm[4][TQ], wl[4][TQ];
   __shared__ float wo[4][TQ][64];
@@ -463,32 +599,66 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
   const int sub = lane & 15, grp = lane >> 4;
   const int kv_len = state ? state->kv_len : kv_len_host;
   const size_t hb = ((size_t)b * H + head) * ctx * 64;
-  // append the new keys / values (decoder.rs:77-112 via Tensor::cat)
-  if (tid < Tq * 16) {
-    const int t = tid >> 4, s4 = (tid & 15) * 4;
-    const float* src = qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + s4;
-    *reinterpret_cast<floatx4*>(ck + hb + (size_t)(kv_len + t) * 64 + s4) = *reinterpret_cast<const floatx4*>(src + D);
-    *reinterpret_cast<floatx4*>(cv + hb + (size_t)(kv_len + t) * 64 + s4) =
-        *reinterpret_cast<const floatx4*>(src + 2 * D);
-  }
   floatx4 qv[TQ];
-#pragma unroll
-  for (int t = 0; t < TQ; ++t)
-    qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + sub * 4) *
-                         kEaQScale
-                   : floatx4{0.f, 0.f, 0.f, 0.f};
-  const int nk = kv_len + Tq;
-  const int per_wave = (nk + 3) / 4;
-  const int k0 = min(nk, wave * per_wave), k1 = min(nk, k0 + per_wave);
   const float* kb = ck + hb + sub * 4;
   const float* vb = cv + hb + sub * 4;
   const float* newb = qkv + (size_t)b * Tq * 3 * D + D + head * 64 + sub * 4;
+  if constexpr (FUSE) {
+    __shared__ float xs[TQ][kXkvMaxD];
+    __shared__ float qs[TQ][64];
+    const size_t wofs = (size_t)head * 64 * (D / 32) * 18;
+    uint32_t w[3][kXkvPairs][9];
+    q4_rows_load(fz.wq + wofs, D, tid, w[0]);
+    q4_rows_load(fz.wk + wofs, D, tid, w[1]);
+    q4_rows_load(fz.wv + wofs, D, tid, w[2]);
+    xkv_ln_rows<TQ>(fz.x, fz.ln_w, fz.ln_b, b, Tq, D, wave, lane, xs);
+    __syncthreads();
+    const int c = tid >> 2;
+#pragma unroll
+    for (int P = 0; P < 3; ++P) {
+      float acc[TQ];
+      q4_rows_dot<TQ>(w[P], D, tid, Tq, xs, acc);
+      if ((tid & 3) == 0) {
+        const float bias = fz.bqkv[P * D + head * 64 + c];
+#pragma unroll
+        for (int t = 0; t < TQ; ++t) {
+          if (t < Tq) {  // append the new keys / values (decoder.rs:77-112 via Tensor::cat)
+            const float val = acc[t] + bias;
+            if (P == 0) qs[t][c] = val;
+            else (P == 1 ? ck : cv)[hb + (size_t)(kv_len + t) * 64 + c] = val;
+          }
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < TQ; ++t)
+      qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(&qs[t][sub * 4]) * kEaQScale : floatx4{0.f, 0.f, 0.f, 0.f};
+  } else {
+    // append the new keys / values (decoder.rs:77-112 via Tensor::cat)
+    if (tid < Tq * 16) {
+      const int t = tid >> 4, s4 = (tid & 15) * 4;
+      const float* src = qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + s4;
+      *reinterpret_cast<floatx4*>(ck + hb + (size_t)(kv_len + t) * 64 + s4) =
+          *reinterpret_cast<const floatx4*>(src + D);
+      *reinterpret_cast<floatx4*>(cv + hb + (size_t)(kv_len + t) * 64 + s4) =
+          *reinterpret_cast<const floatx4*>(src + 2 * D);
+    }
+#pragma unroll
+    for (int t = 0; t < TQ; ++t)
+      qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + sub * 4) *
+                           kEaQScale
+                     : floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int nk = kv_len + Tq;
+  const int per_wave = (nk + 3) / 4;
+  const int k0 = min(nk, wave * per_wave), k1 = min(nk, k0 + per_wave);
   float m[TQ], l[TQ];
   floatx4 o[TQ];
   attn_scan<TQ, 8>(
       qv, Tq, k0, k1, grp,
       [&](int j, const float*& kp, const float*& vp) {
-        if (j < kv_len) {
+        if (FUSE || j < kv_len) {
           kp = kb + (size_t)j * 64;
           vp = vb + (size_t)j * 64;
         } else {  // this step's own keys: not yet visible through the cache
@@ -509,17 +679,24 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
 
 hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float* cache_v, int B, int Tq, int H,
                                          int ctx, const DecodeState* state, int kv_len_host, _Float16* tiled,
-                                         int ns, hipStream_t st) {
+                                         int ns, hipStream_t st, const SelfFuseQkv* fuse) {
   if (Tq > 4 || ctx > kMaxCtx) return hipErrorInvalidValue;
+  if (fuse && (H * 64 > kXkvMaxD || !fuse->x || !fuse->ln_w || !fuse->ln_b || !fuse->wq || !fuse->wk ||
+               !fuse->wv || !fuse->bqkv))
+    return hipErrorInvalidValue;
+  const SelfFuseQkv fz = fuse ? *fuse : SelfFuseQkv{};
   const dim3 grid(H, B), block(256);
-#define WA_SELF(NS_, TQ_)                                                                                      \
-  hipLaunchKernelGGL((dec_self_attn_kernel<NS_, TQ_>), grid, block, 0, st, qkv, cache_k, cache_v, Tq, H, ctx, \
-                     state, kv_len_host, tiled)
+#define WA_SELF(NS_, TQ_, F_)                                                                                    \
+  hipLaunchKernelGGL((dec_self_attn_kernel<NS_, TQ_, F_>), grid, block, 0, st, qkv, cache_k, cache_v, Tq, H, ctx, \
+                     state, kv_len_host, tiled, fz)
+#define WA_SELF2(NS_, TQ_) \
+  if (fuse) WA_SELF(NS_, TQ_, true); else WA_SELF(NS_, TQ_, false)
   if (ns == 2) {
-    if (Tq == 1) WA_SELF(2, 1); else WA_SELF(2, 4);
+    if (Tq == 1) { WA_SELF2(2, 1); } else { WA_SELF2(2, 4); }
   } else {
-    if (Tq == 1) WA_SELF(1, 1); else WA_SELF(1, 4);
+    if (Tq == 1) { WA_SELF2(1, 1); } else { WA_SELF2(1, 4); }
   }
+#undef WA_SELF2
 #undef WA_SELF
   return hipGetLastError();
 }
@@ -556,12 +733,18 @@ int cross_attention_kv_splits(int T) {
   return s < 1 ? 1 : (s > kXkvMaxSplit ? kXkvMaxSplit : s);
 }
 
-template <int NS, int TQ>
+// FUSEQ: the query projection runs inside the kernel (one clip's decode
+// step is a chain of launches, and this removes one): each workgroup forms
+// LN(x) of its clip's Tq rows (cross_attn_ln) and q of its head's 64 columns
+// (q4_rows_load / q4_rows_dot above) while the first pass of K / V loads is
+// already in flight.
+template <int NS, int TQ, bool FUSEQ>
 __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restrict__ q, const float* __restrict__ kc,
                                                             const float* __restrict__ vc, int Tq_, int T, int H,
                                                             int S, float* __restrict__ part,
                                                             int* __restrict__ counters,
-                                                            _Float16* __restrict__ tiled) {
+                                                            _Float16* __restrict__ tiled, XkvFuseQ fq) {
+  constexpr int U = TQ == 1 ? 12 : 8;  // <= 48 keys per wave in flight at once (decode step)
   const int Tq = TQ == 1 ? 1 : Tq_;
   __shared__ float wm[4][TQ], wl[4][TQ];
   __shared__ float wo[4][TQ][64];
@@ -570,11 +753,6 @@ __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restr
   const int head = blockIdx.x / S, split = blockIdx.x - head * S, b = blockIdx.y;
   const int D = H * 64;
   const int sub = lane & 15, grp = lane >> 4;
-  floatx4 qv[TQ];
-#pragma unroll
-  for (int t = 0; t < TQ; ++t)
-    qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(q + (size_t)(b * Tq + t) * D + head * 64 + sub * 4) * kEaQScale
-                   : floatx4{0.f, 0.f, 0.f, 0.f};
   const int per_split = (T + S - 1) / S;
   const int s0 = min(T, split * per_split), s1 = min(T, s0 + per_split);
   const int per_wave = (s1 - s0 + 3) / 4;
@@ -582,15 +760,48 @@ __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restr
   const size_t hofs = ((size_t)b * H + head) * T * 64 + sub * 4;
   const float* kb = kc + hofs;
   const float* vb = vc + hofs;
+  auto rows = [&](int j, const float*& kp, const float*& vp) {
+    kp = kb + (size_t)j * 64;
+    vp = vb + (size_t)j * 64;
+  };
   float m[TQ], l[TQ];
   floatx4 o[TQ];
-  attn_scan<TQ, TQ == 1 ? 12 : 8>(  // <= 48 keys per wave in flight at once (decode step)
-      qv, Tq, k0, k1, grp,
-      [&](int j, const float*& kp, const float*& vp) {
-        kp = kb + (size_t)j * 64;
-        vp = vb + (size_t)j * 64;
-      },
-      [](int, int) { return true; }, m, l, o);
+  floatx4 qv[TQ];
+  attn_init<TQ>(m, l, o);
+  int j0 = k0;
+  if constexpr (FUSEQ) {
+    __shared__ float xs[TQ][kXkvMaxD];
+    __shared__ float qs[TQ][64];
+    const int c = tid >> 2;
+    uint32_t w[kXkvPairs][9];
+    q4_rows_load(fq.wq + (size_t)head * 64 * (D / 32) * 18, D, tid, w);
+    floatx4 kk[U], vv[U];  // the first pass of K / V, before q exists
+    attn_fetch<U>(j0, k1, grp, rows, kk, vv);
+    xkv_ln_rows<TQ>(fq.x, fq.ln_w, fq.ln_b, b, Tq, D, wave, lane, xs);
+    __syncthreads();
+    float acc[TQ];
+    q4_rows_dot<TQ>(w, D, tid, Tq, xs, acc);
+#pragma unroll
+    for (int t = 0; t < TQ; ++t)
+      if ((tid & 3) == 0 && t < Tq) qs[t][c] = acc[t] + fq.bq[head * 64 + c];
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < TQ; ++t)
+      qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(&qs[t][sub * 4]) * kEaQScale : floatx4{0.f, 0.f, 0.f, 0.f};
+    if (j0 < k1) attn_update<TQ, U>(qv, Tq, j0, k1, grp, [](int, int) { return true; }, kk, vv, m, l, o);
+    j0 += 4 * U;
+  } else {
+#pragma unroll
+    for (int t = 0; t < TQ; ++t)
+      qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(q + (size_t)(b * Tq + t) * D + head * 64 + sub * 4) *
+                           kEaQScale
+                     : floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (; j0 < k1; j0 += 4 * U) {
+    floatx4 kk[U], vv[U];
+    attn_fetch<U>(j0, k1, grp, rows, kk, vv);
+    attn_update<TQ, U>(qv, Tq, j0, k1, grp, [](int, int) { return true; }, kk, vv, m, l, o);
+  }
   float mn, ls, os;
   attn_merge<TQ>(Tq, wave, lane, m, l, o, wm, wl, wo, mn, ls, os);
   if (S > 1) {
@@ -652,17 +863,26 @@ size_t cross_attention_kv_part_floats(int B, int H, int T) {
 }
 
 hipError_t launch_cross_attention_kv(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
-                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st) {
+                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st,
+                                     const XkvFuseQ* fuse) {
   if (Tq < 1 || Tq > 4 || B < 1 || T < 1 || H < 1) return hipErrorInvalidValue;
+  if (fuse && (H * 64 > kXkvMaxD || (H * 64) / 64 > 4 * kXkvPairs || !fuse->x || !fuse->ln_w || !fuse->ln_b ||
+               !fuse->wq || !fuse->bq))
+    return hipErrorInvalidValue;
+  const XkvFuseQ fq = fuse ? *fuse : XkvFuseQ{};
   const int S = cross_attention_kv_splits(T);
   const dim3 grid(H * S, B), block(256);
-#define WA_XKV(NS_, TQ_) \
-  hipLaunchKernelGGL((cross_attn_kv_kernel<NS_, TQ_>), grid, block, 0, st, q, k, v, Tq, T, H, S, part, counters, tiled)
+#define WA_XKV(NS_, TQ_, F_)                                                                                 \
+  hipLaunchKernelGGL((cross_attn_kv_kernel<NS_, TQ_, F_>), grid, block, 0, st, q, k, v, Tq, T, H, S, part, \
+                     counters, tiled, fq)
+#define WA_XKV2(NS_, TQ_) \
+  if (fuse) WA_XKV(NS_, TQ_, true); else WA_XKV(NS_, TQ_, false)
   if (ns == 2) {
-    if (Tq == 1) WA_XKV(2, 1); else WA_XKV(2, 4);
+    if (Tq == 1) { WA_XKV2(2, 1); } else { WA_XKV2(2, 4); }
   } else {
-    if (Tq == 1) WA_XKV(1, 1); else WA_XKV(1, 4);
+    if (Tq == 1) { WA_XKV2(1, 1); } else { WA_XKV2(1, 4); }
   }
+#undef WA_XKV2
 #undef WA_XKV
   return hipGetLastError();
 }

@@ -26,9 +26,22 @@ hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Floa
 // appends k, v of the Tq new tokens at cache index kv_len (+ kv_base_extra)
 // and attends over kv_len + Tq entries, causal inside the new tokens when
 // Tq > 1 (attention.rs:270-287).  cache_k/v: [B, ctx, D].
+// With fuse != nullptr (few clips, Q4_0) qkv is not read: each workgroup
+// forms its head's q, k, v from LN(x) (attn_ln) and the raw Q4_0 query / key
+// / value rows [D][D / 32][18 B], bias bqkv [3D] (key part 0).
+struct SelfFuseQkv {
+  const float* x;
+  const float* ln_w;
+  const float* ln_b;
+  const uint8_t* wq;
+  const uint8_t* wk;
+  const uint8_t* wv;
+  const float* bqkv;
+};
 hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float* cache_v, int B, int Tq, int H,
                                          int ctx, const DecodeState* state, int kv_len_host, _Float16* tiled,
-                                         int ns, hipStream_t st);
+                                         int ns, hipStream_t st,
+                                         const SelfFuseQkv* fuse = nullptr);
 
 // Cross-attention over cached K / V (attention.rs:177-236, the reference's
 // form; used for decode groups of a few clips): q [B*Tq, D] f32, k / v
@@ -36,10 +49,20 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
 // output), Tq <= 4; part: cross_attention_kv_part_floats floats, counters:
 // B * H ints zeroed once (re-armed by the kernel).  Writes the A-tiled
 // operand of the output projection.
+// With fuse != nullptr q is not read: the kernel forms it from the residual
+// rows x [B*Tq, D] (q = LN(x) Wq^T + bq, Wq as raw Q4_0 rows, D <= 1280).
+struct XkvFuseQ {
+  const float* x;
+  const float* ln_w;
+  const float* ln_b;
+  const uint8_t* wq;
+  const float* bq;
+};
 int cross_attention_kv_splits(int T);
 size_t cross_attention_kv_part_floats(int B, int H, int T);
 hipError_t launch_cross_attention_kv(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
-                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st);
+                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st,
+                                     const XkvFuseQ* fuse = nullptr);
 
 // Cross-attention over the encoder output (wa_xattn.hip; attention.rs:
 // 204-298 restated without K/V caches): q [B*Tq, D] f32 (rows b*Tq + i),
