@@ -5,6 +5,12 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+Both forms run N ranks: without a torch.distributed.run environment
+(WORLD_SIZE unset) and N > 1, this process starts the N rank processes
+itself (launch_ranks) before anything touches HIP, and exits with the first
+failing rank's status.  `--dry-run` exercises the launch / rendezvous /
+max-over-ranks logic with no GPU work (tests/test_bench_dist.py).
+
 One "step" = one batch of synthetic 30-s clips transcribed end to end on each
 GPU: conv front-end + 32-layer encoder + prompt + greedy KV-cached
 decode (whisper.rs:51-128), mel already resident in HBM, token ids back on the
@@ -13,10 +19,11 @@ the 256-clip / 8-GPU job); each rank runs its own clips (weak scaling, no
 collective on the data path -- one process per GPU, independent replicas).
 value = audio seconds of all ranks' clips / max-over-ranks wall seconds.
 
-roofline: the dominant kernel by GPU time per step (kernel time summed over
-launches; the two decode groups' launches overlap in wall time, so for the
-cross-attention this is summed GPU time, not a share of the wall clock -- the
-same measure as the serial encoder GEMMs' time) -- the Q4 GEMMs (north-star
+roofline: the dominant kernel by WALL time per step -- for the decode
+cross-attention its summed GPU time scaled by the union / sum of its launch
+intervals in the committed kernel trace (profiles/decode_overlap.json: the two
+decode groups' launches overlap), for the serial encoder GEMMs their GPU time
+-- the Q4 GEMMs (north-star
 kernel, MFMA tile kernel, timed live with HIP events on their launch stream
 during the timed steps; algorithmic FLOPs = 2*M*N*K per launch) or the decode
 step's cross-attention (HBM stream of every clip's encoder output, f16 hi/lo
@@ -169,6 +176,39 @@ def in_graph_xattn(rows: int, heads: int, d_model: int, workload: dict):
     return tot
 
 
+def decode_overlap(workload: dict):
+    """The committed wall-time view of the decode (profiles/decode_overlap.json,
+    scripts/decode_overlap.py over the rocprofv3 kernel trace of this
+    workload), or None."""
+    try:
+        with open(os.path.join(REPO, "profiles", "decode_overlap.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return d if d.get("workload") == workload else None
+
+
+def decode_step_bytes(cfg: dict, B: int, groups: int, kv_cache: bool, weights: str, ns: int, kv_avg: float) -> dict:
+    """Algorithmic HBM bytes of one greedy decode step over B clips in `groups`
+    decode groups (each group replays its own step graph, so it streams the
+    weights and the logits table itself), SURVEY §8(d):
+      cross-attention state: every clip's encoder output as f16 planes
+        (ns halves per element) + raw Wk, Wv per group -- or, for few-clip
+        groups, the reference's cached K and V (f32) -- per layer;
+      decoder Q4 weights (qkv, out, cq, cout, fc1, fc2: 14 D^2) per group;
+      self-attention KV cache, K and V f32, kv_avg entries per clip and layer;
+      the tied-embedding logits table (f16 pairs) per group."""
+    D, T, L, V = cfg["n_text_state"], cfg["n_audio_ctx"], cfg["n_text_layer"], cfg["n_vocab"]
+    wb = 2.0 if weights == "f16" else 18.0 / 32.0
+    xattn = B * T * D * 4.0 * 2 if kv_cache else B * T * D * 2.0 * ns + groups * 2 * D * D * wb
+    w = groups * 14 * D * D * wb
+    self_kv = B * kv_avg * D * 4.0 * 2
+    logits = groups * ((V + 127) // 128 * 128) * D * 2.0 * ns
+    per = {"cross_attention": L * xattn, "weights": L * w, "self_kv": L * self_kv, "logits_table": logits}
+    per["total"] = sum(per.values())
+    return per
+
+
 def cpu_threads() -> int:
     """Host cores this process may use: the affinity mask, capped by
     OMP_NUM_THREADS where the box sets it (the GPU box's CPU share)."""
@@ -265,9 +305,83 @@ def cpu_baseline(cfg: dict, rows: int, tokens: float) -> dict:
                           "clip_q4_s_extrapolated": round(cn, 2), "shapes": multi}}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`--gpus N` (N > 1) started without a torch.distributed.run environment:
+    start N rank processes of this script (RANK / WORLD_SIZE / LOCAL_RANK /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT set), one per GPU, and wait for them.
+    This parent never initialises HIP (it imports neither torch nor the
+    product libraries), so no process that touched the GPU is replaced or
+    forks.  If a rank fails, the others are stopped (their exact PIDs) and the
+    failing rank's exit status is returned."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    pending = set(range(n))
+    while pending:
+        for i in sorted(pending):
+            c = procs[i].poll()
+            if c is None:
+                continue
+            pending.discard(i)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench.py: rank {i} exited with status {c}; stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                for j in pending:
+                    procs[j].terminate()
+        time.sleep(0.1)
+    return rc
+
+
+def dry_run(args, rank: int, world: int) -> None:
+    """`--dry-run`: the launch, rendezvous, barrier and max-over-ranks logic of
+    a multi-rank run with no GPU work (the CPU test of `--gpus N`).  Each rank
+    'runs' its clip shard (clip_ids) for a rank-dependent time; rank 0 prints
+    the one JSON line with n_gpus = world."""
+    dist = init_dist() if world > 1 else None
+    ranks_seen = 1
+    if dist is not None:
+        import torch
+
+        t = torch.ones(1, dtype=torch.float64)
+        dist.all_reduce(t)
+        ranks_seen = int(t.item())
+        dist.barrier()
+    t0 = time.perf_counter()
+    ids = clip_ids(rank, args.clips_per_gpu, args.warmup, args.steps)
+    time.sleep(0.01 * (1 + rank))
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist, "cpu")
+    if rank == 0:
+        assert world == args.gpus, f"world size {world} != --gpus {args.gpus}"
+        line = {"metric": METRIC, "value": round(job_rtf(world, args.clips_per_gpu, args.steps, elapsed), 3),
+                "unit": "audio-s/wall-s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(elapsed / args.steps * 1e3, 3), "dry_run": True,
+                "backend": None if dist is None else dist.get_backend(), "ranks_seen": ranks_seen,
+                "clips_rank0": sum(len(s) for s in ids)}
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); > 1 without a torch.distributed.run environment starts them itself")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--variant", default="large_v3", choices=["large_v3", "medium", "tiny_test"])
@@ -286,17 +400,33 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch / rendezvous / max-over-ranks only, no GPU work (CPU test of --gpus N)")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.dry_run:
+        dry_run(args, rank, world)
+        return
     import numpy as np
     import torch
 
     import whisper_amd
     import wq4
 
+    n_dev = wq4.device_count()
+    if n_dev < world:
+        print(f"bench.py: --gpus {world} but {n_dev} HIP device(s) visible", file=sys.stderr, flush=True)
+        sys.exit(2)
     torch.cuda.set_device(local_rank)
     dist = init_dist() if world > 1 else None
     prec = wq4.PREC_F16X2 if args.precision == "f16x2" else wq4.PREC_F16
@@ -417,7 +547,38 @@ def main() -> None:
                    "kernel": f"q4_gemm_decode_kernel (decode-step fc1, split-K, {group_rows} rows)",
                    "avg_us": round(dq["us"], 2),
                    "tflops": round(dq["flops"] / (dq["us"] * 1e-6) * 1e-12, 2)}
-        dominant = roof_xa if roof_xa["gpu_ms_per_step"] > roof_q4["gpu_ms_per_step"] else roof_q4
+        # the decode step as a whole: algorithmic bytes per step / measured wall time per step
+        phase = {k: float(np.mean([t[k] for t in timings])) for k in ("encoder_ms", "cross_kv_ms", "prompt_ms",
+                                                                         "decode_ms")}
+        ns = 2 if prec == wq4.PREC_F16X2 else 1
+        kv_avg = 4.0 + (steps_run + 1) / 2.0  # prompt (4) + the steps so far, averaged over the loop
+        sb = decode_step_bytes(cfg, B, groups, kv, args.weights, ns, kv_avg)
+        step_ms = phase["decode_ms"] / max(1.0, steps_run)
+        ds_gbs = sb["total"] / (step_ms * 1e-3) * 1e-9
+        roof_ds = {"bound": "hbm", "achieved": round(ds_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                   "frac": round(ds_gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                   "kernel": f"one greedy decode step (all {groups} decode groups, {B} clips), wall time",
+                   "ms_per_step": round(step_ms, 4), "bytes_per_step": {k: int(v) for k, v in sb.items()},
+                   "kv_avg": kv_avg, "floor_ms_per_step": round(sb["total"] / (PEAK_HBM_GBS * 1e9) * 1e3, 4)}
+        # wall-time share (like for like with the serial encoder GEMMs): the
+        # groups' launches overlap, so summed GPU time is scaled by the
+        # union / sum of the same family's intervals in the committed trace
+        ov = decode_overlap(workload)
+        fam = None if ov is None else ov["families"].get("cross_attention")
+        roof_xa["wall_ms_per_step"] = None if fam is None else round(roof_xa["gpu_ms_per_step"] * fam["union_over_sum"], 2)
+        main = None if ov is None else ov["families"].get("xattn_main_kernel")
+        if main and not kv:
+            mb = group_rows * cfg["n_audio_ctx"] * cfg["n_text_state"] * 2.0 * ns  # planes per launch
+            cg = mb * main["launches"] / (main["union_us"] * 1e-6) * 1e-9
+            roof_xa["concurrent_main"] = {
+                "source": "profiles/decode_overlap.json", "launches": main["launches"],
+                "sum_us": main["sum_us"], "union_us": main["union_us"], "achieved_gbs": round(cg, 1),
+                "frac": round(cg / PEAK_HBM_GBS, 4),
+                "note": "encoder-plane bytes of every xattn_main launch of both groups over the union of their "
+                        "intervals (wall time with at least one running)"}
+        xa_wall = roof_xa["wall_ms_per_step"] if roof_xa["wall_ms_per_step"] is not None else roof_xa["gpu_ms_per_step"]
+        roof_q4["wall_ms_per_step"] = roof_q4["gpu_ms_per_step"]  # one stream: GPU time is wall time
+        dominant = roof_xa if xa_wall > roof_q4["wall_ms_per_step"] else roof_q4
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "audio-s/wall-s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -433,13 +594,13 @@ def main() -> None:
             "roofline_q4_gemm": roof_q4,
             "roofline_cross_attention": roof_xa,
             "roofline_decode_gemm": roof_dq,
+            "roofline_decode_step": roof_ds,
             "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
                             "tflops": round(v["gflop"] / (v["ms"] * 1e-3) * 1e-3, 2) if v["ms"] else None,
                             "gbs": round(v["gb"] / (v["ms"] * 1e-3), 1) if v["ms"] else None}
                         for k, v in prof.items()},
             "tokens_per_clip": round(mean_tok, 2),
-            "phase_ms": {k: round(float(np.mean([t[k] for t in timings])), 3)
-                         for k in ("encoder_ms", "cross_kv_ms", "prompt_ms", "decode_ms")},
+            "phase_ms": {k: round(v, 3) for k, v in phase.items()},
             "decode_steps": [t["steps"] for t in timings],
             "input": "16 kHz audio in HBM (GPU log-mel timed)" if args.audio else "log-mel in HBM",
             "input_h2d_ms_per_step": round(h2d_s * 1e3, 3),

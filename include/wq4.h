@@ -44,7 +44,9 @@ typedef enum wq4_status {
   WQ4_EBYTES = 3,      /* byte count != N*K/32*18 (tensor.rs:43-48)          */
   WQ4_EHIP = 4,        /* HIP runtime error (launch, memcpy, malloc)         */
   WQ4_ENOMEM = 5,      /* workspace too small / allocation failed            */
-  WQ4_EUNSUPPORTED = 6 /* valid request this build does not implement        */
+  WQ4_EUNSUPPORTED = 6, /* valid request this build does not implement       */
+  WQ4_ERANGE = 7        /* an activation left the MFMA operand range (the
+                           model runtime's overflow guard, whisper_amd.h)   */
 } wq4_status;
 
 /* Activation precision of the product (see header comment).             */
@@ -205,8 +207,9 @@ wq4_status wq4_gemm_ln_tiled(const wq4_tensor* w, const float* bias_dev, const f
  * x * gamma (wq4_atiled_bytes(rows, N, prec)) and, per (row, 16-column
  * tile), the tile mean and sum of squared deviations (stats_out_dev,
  * rows * N/16 * 2 floats).  Consumer (set stats_in_dev, wg_dev): at_dev is
- * that operand; the row statistics are merged (Chan et al., fixed order)
- * and the correction applied before bias / GELU / tiled output; bias_dev is
+ * that operand; the row statistics are merged (the exact equal-count
+ * merge of 16-value tiles, a fixed order: every workgroup gets the same
+ * bits) and the correction applied before bias / GELU / tiled output; bias_dev is
  * W beta + bias and wg_dev W gamma (wq4_ln_fold_vectors).  A launch may be
  * both.  Not bit-identical to wq4_layernorm -> wq4_gemm_tiled (re-associated
  * sums; tolerance in tests/test_q4_gpu.py). */

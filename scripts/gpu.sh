@@ -61,7 +61,8 @@ task_trace() {
   python3 tools/timeline.py "$f" > "$O/timeline.txt" || return 1
   python3 scripts/trace_by_grid.py "$f" "skinny|q4_gemm_decode|xattn|dec_self|logits" "$O/chain_grid.json" > /dev/null || return 1
   python3 scripts/in_graph_summary.py "$O/chain_grid.json" large_v3 q4_0 f16x2 32 "$O/xattn_in_graph.json" || return 1
-  cat "$O/timeline.txt"
+  python3 scripts/decode_overlap.py "$f" large_v3 q4_0 f16x2 32 "$O/decode_overlap.json" > "$O/decode_overlap.log" || return 1
+  cat "$O/timeline.txt" "$O/decode_overlap.log"
   gzip -f "$f"
 }
 
@@ -96,6 +97,31 @@ task_gemm() {
   python3 scripts/mfma_summary.py "$O/gemm_pmc" | tee "$O/q4_gemm_mfma.txt"
 }
 
+# Counter passes over the encoder ring kernel (L geometry, M = 48000) for the
+# product and the encdiag timing builds (1: no scale FMAs, 2: + no dequant):
+# which unit bounds it.  Counters not listed by `rocprofv3 -L` are dropped.
+task_gemmpmc() {
+  cd /tmp
+  timeout -s KILL 60 rocprofv3 -L > "$ROOT/$O/counters.txt" 2>&1
+  local avail; avail=$(grep -oE "\bSQ_[A-Z0-9_]+|\bGRBM_[A-Z0-9_]+|\bTCP_[A-Z0-9_]+" "$ROOT/$O/counters.txt" | sort -u)
+  local P1="SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA GRBM_GUI_ACTIVE"
+  local P2="SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
+  for V in base ${ENCDIAGS:-1 2}; do
+    local LD=""; [ "$V" = base ] || LD="$ROOT/whisper-burn_amd/encdiag/$V"
+    local i=0
+    for P in "$P1" "$P2"; do
+      i=$((i + 1))
+      local C=""; for c in $P; do echo "$avail" | grep -qx "$c" && C="$C $c"; done
+      echo "variant $V pass $i:$C"
+      WQ4_LIB_DIR=$LD ROWS=48000 MODES=${GMODE:-2} ROUNDS=1 REPS=3 timeout -s KILL 120 rocprofv3 --pmc $C \
+        --kernel-include-regex "q4_gemm_enc|prefill" -d "$ROOT/$O/gpmc_${V}_$i" -o run --output-format csv \
+        -- python3 "$ROOT/tools/enc_ab.py" > "$ROOT/$O/gpmc_${V}_$i.log" 2>&1 || { cd "$ROOT"; return 1; }
+      python3 "$ROOT/scripts/mfma_summary.py" "$ROOT/$O/gpmc_${V}_$i" raw | tee -a "$ROOT/$O/gemm_counters.txt"
+    done
+  done
+  cd "$ROOT"
+}
+
 task_groups() {
   for G in ${GLIST:-1 2 3}; do
     WA_DECODE_GROUPS=$G bench_line groups_$G --no-cpu-baseline $BENCH_ARGS || return 1
@@ -112,12 +138,14 @@ task_env() {
   done
 }
 
-task_libs() {
-  local L=${LIB:-libwq4.so}
-  cp whisper-burn_amd/lib/$L /tmp/$L.base
+task_libs() {  # variants load from their own directory (WQ4_LIB_DIR); lib/ is never touched
   for V in base ${VARIANTS} base; do
-    if [ "$V" = base ]; then cp /tmp/$L.base whisper-burn_amd/lib/$L; else cp whisper-burn_amd/diag/$V/$L whisper-burn_amd/lib/$L; fi
-    bench_line lib_$V --no-cpu-baseline $BENCH_ARGS || { cp /tmp/$L.base whisper-burn_amd/lib/$L; return 1; }
+    if [ "$V" = base ]; then
+      bench_line lib_$V --no-cpu-baseline $BENCH_ARGS || return 1
+    else
+      [ -f whisper-burn_amd/diag/$V/libwq4.so ] && [ -f whisper-burn_amd/diag/$V/libwhisper_amd.so ] || { echo "diag/$V incomplete"; return 1; }
+      WQ4_LIB_DIR=$ROOT/whisper-burn_amd/diag/$V bench_line lib_$V --no-cpu-baseline $BENCH_ARGS || return 1
+    fi
   done
 }
 

@@ -92,3 +92,44 @@ def test_bench_group_is_gloo_not_rccl():
     assert [o[2] for o in out] == [3.0, 3.0]
     src = open(os.path.join(REPO, "bench.py")).read()
     assert '"nccl"' not in src and "'nccl'" not in src
+
+
+def _bench_env() -> dict:
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    return env
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`python bench.py --gpus 2` with no torch.distributed.run environment
+    starts 2 rank processes itself (gloo group), and rank 0's one JSON line
+    says n_gpus = 2."""
+    import json
+    import subprocess
+
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "2",
+                          "--warmup", "1", "--clips-per-gpu", "4"], env=_bench_env(), capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(s) for s in out.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2 and line["backend"] == "gloo"
+    assert line["clips_rank0"] == 3 * 4
+    assert line["value"] == pytest.approx(2 * 4 * 2 * 30.0 / (line["ms_per_step"] * 2e-3), rel=1e-2)
+
+
+def test_bench_one_gpu_dry_run_and_mismatch():
+    import json
+    import subprocess
+
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--dry-run"], env=_bench_env(),
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert json.loads(out.stdout.strip().splitlines()[-1])["n_gpus"] == 1
+    # a torch.distributed.run environment that disagrees with --gpus is refused before any GPU call
+    env = dict(_bench_env(), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    bad = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run"], env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert bad.returncode == 2 and "WORLD_SIZE=1" in bad.stderr

@@ -184,6 +184,43 @@ def test_full_size_tokens_f16_precision(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["large_v3_q4", "large_v3_q4_auto", "medium_q4", "large_v3_f16"])
+def test_full_size_tokens_batch_one(name):
+    """BASELINE configs 2 / 3 / 5 pinned directly: every fixture clip
+    transcribed ALONE (B = 1, a model with max_batch 1: one-clip encoder,
+    the one-clip decode group with its cross K/V caches) for the fixture's 224
+    steps; tokens equal the f32 oracle's and the traced logits stay within the
+    bound of test_full_size_tokens_and_logits."""
+    import torch
+
+    import whisper_amd
+    from whisper_oracle import synthetic_mel
+
+    f, meta = _fixture(name)
+    clips, steps, lang = meta["clips"], meta["steps"], meta["lang"]
+    m = whisper_amd.WhisperModel(meta["variant"], meta["seed"], max_batch=1, weights=meta["weights"])
+    n_mels = m.config["n_mels"]
+    ref = f["tokens_f32"]
+    worst = 0.0
+    for b, c in enumerate(clips):
+        mel = torch.from_numpy(synthetic_mel(c, n_mels)[None]).cuda()
+        toks, lg = m.transcribe_trace(mel, f["top_ids"][b:b + 1], lang, steps, eot_stop=False)
+        flips = [(s, int(toks[0][s]), int(ref[b, s]), float(f["margin_f32"][b, s]))
+                 for s in range(steps) if toks[0][s] != ref[b, s]]
+        assert not flips, f"{name} clip {c} alone: {len(flips)} token flips; first {flips[:4]}"
+        got = lg[0, 1:, :].astype(np.float64)
+        r32, r64 = f["top_f32"][b, 1:, :], f["top_f64"][b, 1:, :]
+        for s in range(steps):
+            k = np.isfinite(r64[s])
+            tol = _bound(r32[s, k], r64[s, k])
+            err = float(np.max(np.abs(got[s, k] - r64[s, k])))
+            worst = max(worst, err / tol)
+            assert err <= tol, f"{name} clip {c} alone: step {s + 1}: |gpu - f64| {err:.3e} > {tol:.3e}"
+    print(f"{name} at B = 1: tokens equal ({len(clips)} clips x {steps}), worst logit error {worst:.3f} of the bound")
+    m.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["large_v3_q4", "medium_q4"])
 def test_full_size_tokens_at_bench_shape(name):
     """The bench's own shape pinned to the oracle directly: the fixture's two

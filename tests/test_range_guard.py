@@ -1,0 +1,175 @@
+"""Activation-range guard (layers.rs:12-58, wq4_device.hpp
+split_act): every internal producer feeds the MFMAs f16 pairs of x * 2^4,
+finite for |x| < 4094, where the reference's f32 stays finite far beyond.
+
+Stress fixtures through the whole model (tiny_test, synthetic weights written
+to a GGUF and loaded by the product's loader; the oracle gets the same bytes):
+  * "residual": the decoder's attn.out / cross_attn.out / mlp.2 projections
+    scaled by 3e3, so the decoder residual stream reaches ~1e3-2e4.  The
+    LayerNorm fold feeds that raw stream (x * gamma) to the MFMAs and
+    overflows; the model must notice (non-finite logits flag), re-run on the
+    LayerNorm path (bounded operands) and return the f32 oracle's tokens.
+  * "fc1": decoder layer 0's mlp.0 scaled by 5e3 -- fc1 outputs ~1e3-2e4, the
+    GELU output is fc2's operand: no bounded path exists, so transcribe must
+    FAIL LOUDLY (WQ4_ERANGE), never return tokens from NaN logits.
+The oracle is float32 numpy (oracle/whisper_oracle.py) with a float64 run to
+check the fixture has no near-ties; it also records the activation
+magnitudes the fixture promises (CPU test below)."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import whisper_oracle as wo
+
+SEED = 1234
+STEPS = 24
+CLIPS = (0, 1)
+SCALE = {"residual": 3.0e3, "fc1": 5.0e3}
+
+
+def _scaled_names(kind: str) -> list[str]:
+    if kind == "residual":
+        return [f"decoder.blocks.{i}.{p}.{s}" for i in range(2) for p in ("attn.out", "cross_attn.out", "mlp.2")
+                for s in ("weight", "bias")]
+    return ["decoder.blocks.0.mlp.0.weight", "decoder.blocks.0.mlp.0.bias"]
+
+
+def stress_tensors(kind: str) -> dict[str, np.ndarray]:
+    """The synthetic tiny_test tensors (oracle generator = the product's) with
+    the fixture's tensors scaled by SCALE."""
+    import write_gguf
+
+    out = {}
+    scaled = set(_scaled_names(kind))
+    for name, shape, lo, hi in write_gguf.synthetic_specs("tiny_test"):
+        a = oracle.synth_uniform(SEED, name, int(np.prod(shape)), lo, hi).reshape(shape)
+        out[name] = (a * np.float32(SCALE[kind])).astype(np.float32) if name in scaled else a
+    return out
+
+
+class _Recorder(wo.SynthWhisper):
+    """The oracle, recording max |residual stream| (LayerNorm inputs of the
+    decoder blocks) and max |fc1 output| of the decoder."""
+
+    def __init__(self, *a, **k):
+        self.max_resid = 0.0
+        self.max_fc1 = 0.0
+        super().__init__(*a, **k)
+
+    def layer_norm(self, x, p):
+        if p.startswith("decoder.blocks."):
+            self.max_resid = max(self.max_resid, float(np.max(np.abs(x))))
+        return super().layer_norm(x, p)
+
+    def linear(self, x, p, bias=True):
+        y = super().linear(x, p, bias)
+        if p.startswith("decoder.blocks.") and p.endswith("mlp.0"):
+            self.max_fc1 = max(self.max_fc1, float(np.max(np.abs(y))))
+        return y
+
+
+def stress_oracle(kind: str, dtype=np.float32) -> _Recorder:
+    import write_gguf
+
+    m = _Recorder("tiny_test", SEED, dtype=dtype)
+    t = stress_tensors(kind)
+    for name in _scaled_names(kind):
+        a = t[name]
+        if write_gguf.should_quantize(name, a.shape):
+            q = oracle.quantize_convert_np(a.reshape(-1))
+            m.w[name] = oracle.dequantize_np(q, a.size).reshape(a.shape).astype(dtype)
+        else:
+            m.w[name] = a.astype(dtype)
+    return m
+
+
+def _mels(n_mels: int) -> np.ndarray:
+    return np.stack([wo.synthetic_mel(c, n_mels) for c in CLIPS])
+
+
+_CACHE: dict = {}
+
+
+def oracle_run(kind: str):
+    if kind not in _CACHE:
+        m32 = stress_oracle(kind)
+        mel = _mels(m32.cfg["n_mels"])
+        t32 = m32.transcribe(mel, 50259, STEPS, eot_stop=False)
+        m64 = stress_oracle(kind, np.float64)
+        t64 = m64.transcribe(mel, 50259, STEPS, eot_stop=False)
+        _CACHE[kind] = (t32, t64, m32.max_resid, m32.max_fc1)
+    return _CACHE[kind]
+
+
+@pytest.mark.parametrize("kind", ["residual", "fc1"])
+def test_stress_fixture_reaches_the_range(kind):
+    """CPU: the fixture really drives the activations to 1e3-2e4 (beyond the
+    4094 the f16 pair of x * 2^4 holds), and the f32 oracle's tokens equal the
+    f64 oracle's (no near-ties: the GPU comparison below is meaningful)."""
+    t32, t64, max_resid, max_fc1 = oracle_run(kind)
+    print(f"{kind}: max |residual| {max_resid:.4g}, max |fc1| {max_fc1:.4g}")
+    assert t32 == t64
+    if kind == "residual":
+        assert 4094 < max_resid <= 2e4, max_resid
+        assert max_fc1 < 100, max_fc1
+    else:
+        assert 4094 < max_fc1 <= 2e4, max_fc1
+
+
+def _write(kind: str, tmp_path) -> str:
+    import write_gguf
+
+    p = os.path.join(str(tmp_path), f"stress_{kind}.gguf")
+    write_gguf.write_gguf(p, stress_tensors(kind), f"stress-{kind}", quantize=oracle.quantize_convert_np)
+    return p
+
+
+@pytest.mark.gpu
+def test_residual_overflow_recovers_oracle_tokens(tmp_path):
+    import torch
+
+    import whisper_amd
+
+    t32, _, _, _ = oracle_run("residual")
+    m = whisper_amd.WhisperModel.from_gguf(_write("residual", tmp_path), "tiny_test", max_batch=len(CLIPS))
+    assert not m.wide_range
+    mel = torch.from_numpy(_mels(m.config["n_mels"])).cuda()
+    toks = m.transcribe(mel, 50259, STEPS, eot_stop=False)
+    assert m.wide_range  # the fold overflowed and the transcribe was re-run on the LayerNorm path
+    assert toks == t32
+    toks2 = m.transcribe(mel, 50259, STEPS, eot_stop=False)  # sticky: straight on the LayerNorm path
+    assert toks2 == t32
+    m.close()
+
+
+@pytest.mark.gpu
+def test_fc1_overflow_fails_loudly(tmp_path):
+    import torch
+
+    import whisper_amd
+    import wq4
+
+    m = whisper_amd.WhisperModel.from_gguf(_write("fc1", tmp_path), "tiny_test", max_batch=len(CLIPS))
+    mel = torch.from_numpy(_mels(m.config["n_mels"])).cuda()
+    with pytest.raises(wq4.WQ4Error) as ei:
+        m.transcribe(mel, 50259, STEPS, eot_stop=False)
+    assert ei.value.status == 7 and "activation overflow" in ei.value.msg
+    m.close()
+
+
+@pytest.mark.gpu
+def test_normal_model_never_flags():
+    import torch
+
+    import whisper_amd
+
+    m = whisper_amd.WhisperModel("tiny_test", SEED, max_batch=2)
+    mel = torch.from_numpy(_mels(m.config["n_mels"])).cuda()
+    m.transcribe(mel, 50259, STEPS, eot_stop=False)
+    m.transcribe(mel, None, STEPS, eot_stop=True)
+    assert not m.wide_range
+    m.close()

@@ -1144,7 +1144,7 @@ __device__ __forceinline__ void better(float& bv, int& bi, float v, int i) {
 
 __global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ logits, int V, int lo, int hi,
                                                      int suppress_fixed, int min_tokens, const DecodeState* state,
-                                                     int* __restrict__ out, int out_stride) {
+                                                     int* __restrict__ out, int out_stride, int* __restrict__ range_flag) {
   __shared__ float sv[4];
   __shared__ int si[4];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1152,11 +1152,14 @@ __global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ l
   const int suppress = state ? (state->step + 1 < min_tokens) : suppress_fixed;
   float bv = -INFINITY;
   int bi = -1;
+  bool bad = false;
   for (int i = lo + tid; i < hi; i += 256) {
     float v = lg[i];
+    bad |= !__builtin_isfinite(v);
     if (suppress && i == kEOT) v = -INFINITY;
     better(bv, bi, v, i);
   }
+  if (bad && range_flag) *range_flag = 1;  // plain vector store: every writer stores 1
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float v = __shfl_xor(bv, o, 64);
@@ -1175,16 +1178,17 @@ __global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ l
 }
 
 hipError_t launch_argmax(const float* logits, int B, int V, int lo, int hi, int suppress_eot,
-                         const DecodeState* state, int* out_tok, int out_stride, hipStream_t st) {
+                         const DecodeState* state, int* out_tok, int out_stride, int* range_flag, hipStream_t st) {
   hipLaunchKernelGGL(argmax_kernel, dim3(B), dim3(256), 0, st, logits, V, lo, hi, suppress_eot, 0,
-                     (const DecodeState*)nullptr, out_tok, out_stride);
+                     (const DecodeState*)nullptr, out_tok, out_stride, range_flag);
   (void)state;
   return hipGetLastError();
 }
 
 hipError_t launch_argmax_step(const float* logits, int B, int V, int min_tokens, const DecodeState* state,
-                              int* out_tok, hipStream_t st) {
-  hipLaunchKernelGGL(argmax_kernel, dim3(B), dim3(256), 0, st, logits, V, 0, V, 0, min_tokens, state, out_tok, 1);
+                              int* out_tok, int* range_flag, hipStream_t st) {
+  hipLaunchKernelGGL(argmax_kernel, dim3(B), dim3(256), 0, st, logits, V, 0, V, 0, min_tokens, state, out_tok, 1,
+                     range_flag);
   return hipGetLastError();
 }
 
@@ -1293,7 +1297,7 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
     const _Float16* __restrict__ htiled, int B, int D, const _Float16* __restrict__ emb2, int V, int min_tokens,
     const DecodeState* __restrict__ state, float* __restrict__ pval, int* __restrict__ pidx, int* __restrict__ counter,
     int* __restrict__ out_tok, const int* __restrict__ trace_ids, float* __restrict__ trace_out, int trace_s1,
-    int trace_k) {
+    int trace_k, int* __restrict__ range_flag) {
   constexpr int KS = kLg2Chunk / 32;             // Q4-block-sized k-steps per chunk
   constexpr int HCH = KS * 2 * NS * 1024;        // bytes of hidden fragments per chunk
   static_assert(HCH % (256 * 16) == 0, "whole glds rounds");
@@ -1387,6 +1391,7 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
   }
   // acc[mt][nt]: lane holds clip 16 nt + l16, vocab v0 + 16 mt + 4 lq + j
   const int suppress = state->step + 1 < min_tokens;
+  bool bad = false;
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -1396,9 +1401,13 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
         const int vl = 16 * mt + 4 * lq + j;
         const int n = v0 + vl;
         float v = acc[mt][nt][j] * kLgInv;
+        bad |= n < V && 16 * nt + l16 < B && !__builtin_isfinite(v);
         if (n >= V || (suppress && n == kEOT)) v = -INFINITY;
         lg[(16 * nt + l16) * kLgPickLd + wave * 32 + vl] = v;
       }
+  // an MFMA operand out of the f16-pair range upstream turns every logit of
+  // the clip into inf / NaN: flag it (plain vector store, every writer stores 1)
+  if (bad && range_flag) *range_flag = 1;
   if (trace_out) {  // diagnostics only: uniform branch
     __syncthreads();
     const int slot = state->step + 1;
@@ -1461,15 +1470,15 @@ hipError_t launch_emb_tiled(const float* emb, int V, int D, int ns, _Float16* ou
 hipError_t launch_logits_argmax(const _Float16* htiled, int B, int D, const _Float16* emb2, int ns, int V,
                                 int min_tokens, const DecodeState* state, float* pval, int* pidx, int* counter,
                                 int* out_tok, const int* trace_ids, float* trace_out, int trace_s1, int trace_k,
-                                hipStream_t st) {
+                                int* range_flag, hipStream_t st) {
   if (B < 1 || B > 32 || !emb_tiled_supported(D) || !state || !emb2 || !htiled) return hipErrorInvalidValue;
   const dim3 grid(logits_argmax_groups(V));
   if (ns == 2)
     hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<2>, grid, dim3(256), 0, st, htiled, B, D, emb2, V, min_tokens,
-                       state, pval, pidx, counter, out_tok, trace_ids, trace_out, trace_s1, trace_k);
+                       state, pval, pidx, counter, out_tok, trace_ids, trace_out, trace_s1, trace_k, range_flag);
   else
     hipLaunchKernelGGL(logits_argmax_f16_k32_kernel<1>, grid, dim3(256), 0, st, htiled, B, D, emb2, V, min_tokens,
-                       state, pval, pidx, counter, out_tok, trace_ids, trace_out, trace_s1, trace_k);
+                       state, pval, pidx, counter, out_tok, trace_ids, trace_out, trace_s1, trace_k, range_flag);
   return hipGetLastError();
 }
 

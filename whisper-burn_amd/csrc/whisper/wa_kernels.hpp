@@ -118,8 +118,11 @@ hipError_t launch_logits(const float* h, int B, int D, long ldh, const float* em
 // maximum winning ties (Rust max_by), EOT (50257) masked when suppress != 0,
 // or restricted to [lo, hi) for language detection (whisper.rs:76-83).
 // Writes out_tok[b * out_stride].
+// range_flag (nullable): set to 1 when a logit of [lo, hi) is not finite --
+// an MFMA operand left the f16-pair range somewhere upstream (the
+// overflow propagates to every logit of the clip); wa_transcribe checks it.
 hipError_t launch_argmax(const float* logits, int B, int V, int lo, int hi, int suppress_eot,
-                         const DecodeState* state, int* out_tok, int out_stride, hipStream_t st);
+                         const DecodeState* state, int* out_tok, int out_stride, int* range_flag, hipStream_t st);
 
 // Decode-step logits fused with the greedy pick (launch_logits +
 // launch_argmax_step in one kernel, logits never stored): B <= 32 rows,
@@ -131,10 +134,11 @@ int logits_argmax_groups(int V);
 // table, fragment-tiled (launch_emb_tiled); D % 128 == 0.
 // trace_ids / trace_out (diagnostics; null in the product): [B][trace_s1]
 // [trace_k] -- the logits of the listed ids at slot state->step + 1.
+// range_flag (nullable): as launch_argmax, for every logit of the B rows.
 hipError_t launch_logits_argmax(const _Float16* htiled, int B, int D, const _Float16* emb2, int ns, int V,
                                 int min_tokens, const DecodeState* state, float* pval, int* pidx, int* counter,
                                 int* out_tok, const int* trace_ids, float* trace_out, int trace_s1, int trace_k,
-                                hipStream_t st);
+                                int* range_flag, hipStream_t st);
 // Whether the logits kernel reads a fragment-tiled table for this width.
 bool emb_tiled_supported(int D);
 // Rows of the fragment-tiled table (V padded to the kernel's 128-row groups).
@@ -157,6 +161,6 @@ hipError_t launch_bookkeep(const int* next_tok, int* tokens, int* n_tokens, int*
 // Step-dependent EOT suppression (whisper.rs:120-122) folded into argmax:
 // suppress iff state->step < min_tokens - 1 (state->step already advanced).
 hipError_t launch_argmax_step(const float* logits, int B, int V, int min_tokens, const DecodeState* state,
-                              int* out_tok, hipStream_t st);
+                              int* out_tok, int* range_flag, hipStream_t st);
 
 }  // namespace wa

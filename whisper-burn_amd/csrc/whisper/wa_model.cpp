@@ -233,6 +233,16 @@ struct wa_model {
   int kv_n = 0;
   bool group_kv(const DecGroup& g) const { return g.nb > 0 && g.b0 + g.nb <= kv_n; }
   hipStream_t own_stream = nullptr;  // encoder / encoder planes (graph capture needs a non-null stream)
+  // Activation-range guard.  Every internal producer writes MFMA operands as
+  // f16 pairs of x * 2^4 (wq4_device.hpp split_act), finite for |x| < 4094;
+  // beyond that the f16 half overflows and the clip's logits become inf /
+  // NaN.  The pick kernels set *range_flag on any non-finite logit.  After a
+  // flagged transcribe the model retries it once with the LayerNorm fold off
+  // (wide_range: the fold feeds the RAW residual stream x * gamma to the MFMAs,
+  // where the LayerNorm path feeds LayerNorm(x), bounded by sqrt(D) |gamma| +
+  // |beta|); still flagged -> WQ4_ERANGE, never NaN tokens.
+  int* range_flag = nullptr;
+  bool wide_range = false;
   float timings[5] = {0, 0, 0, 0, 0};
   // decode-step logit trace (wa_transcribe_trace; null otherwise): device
   // [clip][trace_s1][trace_k] ids and their logits
@@ -730,8 +740,11 @@ wq4_status alloc_activations(wa_model* m) {
     WA_HIP(hipHostMalloc(reinterpret_cast<void**>(&g.host_ndone), 8 * sizeof(int), 0));
     WA_HIP(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
   }
-  for (void* p : {(void*)m->h1, (void*)m->x, (void*)m->qkv, (void*)m->at_d, (void*)m->at_f, (void*)m->enc_planes})
+  m->range_flag = d.alloc<int>(1);
+  for (void* p : {(void*)m->h1, (void*)m->x, (void*)m->qkv, (void*)m->at_d, (void*)m->at_f, (void*)m->enc_planes,
+                  (void*)m->range_flag})
     if (!p) return fail(WQ4_ENOMEM, "activation allocation failed");
+  WA_HIP(hipMemset(m->range_flag, 0, sizeof(int)));
   for (auto& L : m->dec)
     if (!L.cache_k || !L.cache_v) return fail(WQ4_ENOMEM, "KV cache allocation failed");
   // zero the A-tiled buffers once: padded rows stay finite forever
@@ -862,7 +875,7 @@ bool lnfold_on(const wa_model* m, int Tq, const wa::DecodeState* state, int64_t 
     const char* e = getenv("WA_LN_FOLD");
     return e ? atoi(e) != 0 : true;
   }();
-  if (!enabled || state == nullptr || Tq != 1 || m->dec.empty()) return false;
+  if (!enabled || m->wide_range || state == nullptr || Tq != 1 || m->dec.empty()) return false;
   const DecLayer& L = m->dec[0];
   for (const wq4_tensor* w : {L.qkv, L.out, L.cq, L.cout, L.fc1, L.fc2})
     if (!wq4_lnfold_supported(w, rows)) return false;
@@ -973,7 +986,8 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
     const size_t tofs = (size_t)g.b0 * m->trace_s1 * m->trace_k;
     WA_HIP(wa::launch_logits_argmax(g.hid_t, B, D, m->tok_emb2, m->ns, c.n_vocab, kMinTokens, state, g.lg_val,
                                     g.lg_idx, g.lg_ctr, g.next_tok, m->trace_out ? m->trace_ids + tofs : nullptr,
-                                    m->trace_out ? m->trace_out + tofs : nullptr, m->trace_s1, m->trace_k, st));
+                                    m->trace_out ? m->trace_out + tofs : nullptr, m->trace_s1, m->trace_k,
+                                    m->range_flag, st));
     return WQ4_OK;
   }
   WA_WQ4(wq4_layernorm(g.xd, m->dln_w, m->dln_b, rows, D, WQ4_PREC_F16X2, nullptr, g.hid, st));
@@ -988,7 +1002,7 @@ wq4_status decode_step(wa_model* m, DecGroup& g, int eot_stop, hipStream_t st) {
   wq4_status s = decoder_forward(m, g, g.next_tok, 1, g.state, 0, 0, st);
   if (s != WQ4_OK) return s;
   if (!fused_pick(g, 1, g.state))
-    WA_HIP(wa::launch_argmax_step(g.logits, g.nb, m->cfg.n_vocab, kMinTokens, g.state, g.next_tok, st));
+    WA_HIP(wa::launch_argmax_step(g.logits, g.nb, m->cfg.n_vocab, kMinTokens, g.state, g.next_tok, m->range_flag, st));
   return WQ4_OK;
 }
 
@@ -1027,7 +1041,8 @@ wq4_status prompt_group(wa_model* m, DecGroup& g, int lang_token, hipStream_t st
     WA_HIP(hipMemcpyAsync(g.next_tok, sot.data(), (size_t)B * 4, hipMemcpyHostToDevice, st));
     s = decoder_forward(m, g, g.next_tok, 1, nullptr, 0, 0, st);
     if (s != WQ4_OK) return s;
-    WA_HIP(wa::launch_argmax(g.logits, B, c.n_vocab, 50259, 50259 + c.n_lang, 0, nullptr, g.prompt_tok, 3, st));
+    WA_HIP(wa::launch_argmax(g.logits, B, c.n_vocab, 50259, 50259 + c.n_lang, 0, nullptr, g.prompt_tok, 3,
+                             m->range_flag, st));
     // ... then forward_prompt([lang, TRANSCRIBE, NO_TIMESTAMPS]) OVERWRITES the
     // cache from index 0 with positions 0..2 (decoder.rs:272-283) while the
     // position counter continues at 1 + 3 = 4 (whisper.rs:74,93).
@@ -1037,7 +1052,7 @@ wq4_status prompt_group(wa_model* m, DecGroup& g, int lang_token, hipStream_t st
     kv0 = 3;
   }
   // first token: EOT suppressed (whisper.rs:97-99)
-  WA_HIP(wa::launch_argmax(g.logits, B, c.n_vocab, 0, c.n_vocab, 1, nullptr, g.next_tok, 1, st));
+  WA_HIP(wa::launch_argmax(g.logits, B, c.n_vocab, 0, c.n_vocab, 1, nullptr, g.next_tok, 1, m->range_flag, st));
   const wa::DecodeState init{pos0 - 1, kv0 - 1, -1, 0};
   WA_HIP(hipMemcpyAsync(g.state, &init, sizeof(init), hipMemcpyHostToDevice, st));
   WA_HIP(hipMemsetAsync(g.ntok, 0, (size_t)B * 4, st));
@@ -1051,8 +1066,8 @@ wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
   // everything the captured step bakes in: the clip range (self-KV and
   // encoder-plane offsets), the EOT mode and the trace buffers
   const int64_t key =
-      ((((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0)) * 2 +
-      (m->group_kv(g) ? 1 : 0);
+      (((((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0)) * 2 +
+       (m->group_kv(g) ? 1 : 0)) * 2 + (m->wide_range ? 1 : 0);
   if (g.graph && g.graph_key == key) return WQ4_OK;
   if (g.graph) {
     (void)hipGraphExecDestroy(g.graph);
@@ -1297,12 +1312,14 @@ wq4_status wa_prompt_logits(wa_model* m, const int32_t* prompt_dev, int n_clips,
   return WQ4_OK;
 }
 
-wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lang_token, int max_tokens,
-                         int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out, void* stream) {
-  if (!m || !mel_dev || !tokens_out || !n_tokens_out) return fail(WQ4_EINVAL, "null argument");
-  if (n_clips < 1 || n_clips > m->bmax) return fail(WQ4_EINVAL, "n_clips out of range");
-  if (max_tokens < 1 || max_tokens > kMaxTokens) return fail(WQ4_EINVAL, "max_tokens must be in [1, 224]");
-  WA_HIP(hipSetDevice(m->device));
+}  // extern "C"
+
+namespace {
+
+// One transcribe (whisper.rs:51-128 for a batch of clips); *overflow = the
+// range flag of this run (see wa_model::range_flag).
+wq4_status transcribe_once(wa_model* m, const float* mel_dev, int n_clips, int lang_token, int max_tokens,
+                           int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out, void* stream, bool* overflow) {
   // all work on the model's own stream, ordered after the caller's stream
   hipStream_t st = m->own_stream;
   const int B = n_clips;
@@ -1316,6 +1333,7 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
   } evg{ev};
   WA_HIP(hipEventRecord(ev[4], static_cast<hipStream_t>(stream)));
   WA_HIP(hipStreamWaitEvent(st, ev[4], 0));
+  WA_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
 
   WA_HIP(hipEventRecord(ev[0], st));
   wq4_status s = encoder_forward(m, mel_dev, B, st, nullptr);
@@ -1415,7 +1433,10 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
                           hipMemcpyDeviceToHost, st));
     WA_HIP(hipMemcpyAsync(nt.data() + g.b0, g.ntok, (size_t)g.nb * 4, hipMemcpyDeviceToHost, st));
   }
+  int flag = 0;
+  WA_HIP(hipMemcpyAsync(&flag, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
   WA_HIP(hipStreamSynchronize(st));
+  *overflow = flag != 0;
   for (int b = 0; b < B; ++b) {
     n_tokens_out[b] = std::min(nt[b], max_tokens);
     std::memcpy(tokens_out + (size_t)b * max_tokens, tok.data() + (size_t)b * kMaxTokens,
@@ -1437,6 +1458,38 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
   m->timings[4] = (float)steps;
   return WQ4_OK;
 }
+
+}  // namespace
+
+extern "C" {
+
+wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lang_token, int max_tokens,
+                         int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out, void* stream) {
+  if (!m || !mel_dev || !tokens_out || !n_tokens_out) return fail(WQ4_EINVAL, "null argument");
+  if (n_clips < 1 || n_clips > m->bmax) return fail(WQ4_EINVAL, "n_clips out of range");
+  if (max_tokens < 1 || max_tokens > kMaxTokens) return fail(WQ4_EINVAL, "max_tokens must be in [1, 224]");
+  WA_HIP(hipSetDevice(m->device));
+  bool overflow = false;
+  wq4_status s = transcribe_once(m, mel_dev, n_clips, lang_token, max_tokens, eot_stop, tokens_out, n_tokens_out,
+                                 stream, &overflow);
+  if (s != WQ4_OK) return s;
+  if (overflow && !m->wide_range) {
+    // the LayerNorm fold feeds the raw residual stream to the MFMAs: retry on
+    // the LayerNorm path, and keep it for this model (sticky: its activations
+    // evidently exceed the fold's range)
+    m->wide_range = true;
+    s = transcribe_once(m, mel_dev, n_clips, lang_token, max_tokens, eot_stop, tokens_out, n_tokens_out, stream,
+                        &overflow);
+    if (s != WQ4_OK) return s;
+  }
+  if (overflow)
+    return fail(WQ4_ERANGE,
+                "activation overflow: an MFMA operand left the f16-pair range (|x| >= 4094 after the LayerNorm, "
+                "GELU or attention producers) and the logits are not finite");
+  return WQ4_OK;
+}
+
+int wa_model_wide_range(const wa_model* m) { return m ? (m->wide_range ? 1 : 0) : -1; }
 
 wq4_status wa_transcribe_trace(wa_model* m, const float* mel_dev, int n_clips, int lang_token, int max_tokens,
                                int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out, const int32_t* trace_ids_dev,
@@ -1675,7 +1728,7 @@ wq4_status wa_logits_argmax_check(int device, const float* hid_dev, const float*
     if (!tr) return fail(WQ4_ENOMEM, "allocation failed");
   }
   WA_HIP(wa::launch_logits_argmax(ht, n_clips, D, emb2, ns, V, min_tokens, st, pval, pidx, ctr, tok_dev,
-                                  ids, tr, 2, V, nullptr));
+                                  ids, tr, 2, V, nullptr, nullptr));
   if (logits_dev)
     for (int b = 0; b < n_clips; ++b)
       WA_HIP(hipMemcpy(logits_dev + (size_t)b * V, tr + ((size_t)b * 2 + 1) * V, (size_t)V * 4,

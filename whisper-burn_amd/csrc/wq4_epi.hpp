@@ -31,7 +31,8 @@ struct EpiArgs {
   // pairs) and per (row, 16-column tile) the tile mean and sum of squared
   // deviations (lnf_stats_out [M][N/16][2]).
   // Consumer (a GEMM on LayerNorm(x)): A = tiled(x * gamma); merges the
-  // lnf_tiles tile statistics of each row (Chan et al.) and applies
+  // lnf_tiles tile statistics of each row (exact equal-count merge of
+  // 16-value tiles, wq4_lnmath.hpp lnf_merge_tiles) and applies
   // out = (acc - mean * lnf_wg[n]) / sqrt(var + 1e-5) + bias[n] before the
   // rest of the epilogue (bias = W beta + linear bias, lnf_wg = W gamma).
   const float* lnf_g;

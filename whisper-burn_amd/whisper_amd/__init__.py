@@ -53,6 +53,8 @@ def lib() -> ctypes.CDLL:
                                                    ctypes.POINTER(vp)]
         L.wa_model_weight_type.argtypes = [vp]
         L.wa_model_weight_type.restype = c_int
+        L.wa_model_wide_range.argtypes = [vp]
+        L.wa_model_wide_range.restype = c_int
         L.wa_model_create_from_gguf.argtypes = [c_int, ctypes.c_char_p, c_int, c_int, c_int, ctypes.POINTER(vp)]
         L.wa_gguf_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
         L.wa_gguf_close.argtypes = [vp]
@@ -304,6 +306,12 @@ class WhisperModel:
                   precision: int = wq4.PREC_F16X2) -> "WhisperModel":
         """load_whisper_from_gguf (src/gguf/loader.rs:26-45)."""
         return cls(variant, 0, max_batch, device, precision, gguf_path=path)
+
+    @property
+    def wide_range(self) -> bool:
+        """True once a transcribe overflowed the LayerNorm fold's operand range
+        and the model switched to the LayerNorm path (wa_model_wide_range)."""
+        return lib().wa_model_wide_range(self._h) == 1
 
     def device_bytes(self) -> int:
         return int(lib().wa_model_device_bytes(self._h))

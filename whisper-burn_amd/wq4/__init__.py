@@ -26,7 +26,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_PKG_ROOT), "include", "wq4.h")
 
 WQ4_OK = 0
 STATUS_NAMES = {0: "WQ4_OK", 1: "WQ4_EINVAL", 2: "WQ4_ESHAPE", 3: "WQ4_EBYTES", 4: "WQ4_EHIP", 5: "WQ4_ENOMEM",
-                6: "WQ4_EUNSUPPORTED"}
+                6: "WQ4_EUNSUPPORTED", 7: "WQ4_ERANGE"}
 PREC_F16X2 = 0
 PREC_F16 = 1
 EPI_GELU = 1
