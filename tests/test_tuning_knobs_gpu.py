@@ -5,9 +5,8 @@ decode-GEMM plan (wq4_q4gemm.hip plan_decode: WQ4_DECODE_W8, _PER8, _PER,
 _MAXKS), the LayerNorm fold off (wa_model.cpp lnfold_on: WA_LN_FOLD),
 another number of decode groups (wa_model.cpp decode_groups:
 WA_DECODE_GROUPS) or the cross-attention over cached K / V for more clips
-(wa_model.cpp kv_config: WA_XATTN_KV_CLIPS; its query projection inside
-the launch or not: WA_XKV_FUSEQ; the self-attention's q / k / v likewise:
-WA_SELF_FUSE) -- so the greedy tokens of 16 synthetic tiny_test clips
+(wa_model.cpp kv_config: WA_XATTN_KV_CLIPS, whose groups then also form
+their qkv / query projections inside the attention launches) -- so the greedy tokens of 16 synthetic tiny_test clips
 must equal the default's, and a sample must equal the oracle's
 (oracle/whisper_oracle.py).  The knobs are read once per process, so each
 setting runs tests/knob_child.py in a child interpreter.
@@ -38,15 +37,13 @@ KNOBS = [
     {"WA_DECODE_GROUPS": "3"},                            # ragged groups 6/5/5
     {"WA_XATTN_KV_CLIPS": "16"},                          # cross K/V caches, two groups of 8
     {"WA_XATTN_KV_CLIPS": "16", "WA_DECODE_GROUPS": "3"},  # ... at ragged group offsets
-    {"WA_XATTN_KV_CLIPS": "16", "WA_XKV_FUSEQ": "1"},     # ... its query projection inside the launch
-    {"WA_XATTN_KV_CLIPS": "16", "WA_XKV_FUSEQ": "1", "WA_SELF_FUSE": "1"},  # ... and the self-attention's q / k / v
 ]
 
 
 def _run(env_over):
     env = dict(os.environ)
     for k in ("WQ4_DECODE_W8", "WQ4_DECODE_PER8", "WQ4_DECODE_PER", "WQ4_DECODE_MAXKS", "WA_LN_FOLD",
-              "WA_DECODE_GROUPS", "WA_XATTN_KV_CLIPS", "WA_XKV_FUSEQ", "WA_SELF_FUSE"):
+              "WA_DECODE_GROUPS", "WA_XATTN_KV_CLIPS"):
         env.pop(k, None)
     env.update(env_over)
     r = subprocess.run([sys.executable, os.path.join(HERE, "knob_child.py")], env=env, capture_output=True,

@@ -168,49 +168,3 @@ def test_xattn_kv_cache_form(torch, B, Tq, T, H):
     # 2^-22 f16 pair (the output projection's operand) and read back
     err = np.abs(got - ref).max() / np.abs(v).max()
     assert err <= 2e-6, err
-
-
-@pytest.mark.parametrize("B,Tq,T,H", [
-    (1, 1, 1500, 20),   # Large-V3, one clip: the product's default few-clip form
-    (2, 4, 1500, 20),   # prompt rows
-    (8, 1, 1500, 16),   # Medium, the largest few-clip group
-    (3, 3, 37, 6),      # short T, a narrow model (block pairs past the row)
-])
-def test_xattn_kv_fused_query(torch, B, Tq, T, H):
-    """cross_attn_kv_kernel with the query projection inside the launch
-    (FUSEQ): q = LN(x) Wq^T + bq from raw GGUF Q4_0 rows, then softmax(q K^T /
-    8) V -- against float64 of the same dequantised weights."""
-    import whisper_amd
-
-    rng = np.random.default_rng(7000 + B * 100 + Tq * 10 + H)
-    D = 64 * H
-    x = (3.0 * rng.standard_normal((B * Tq, D)) + 0.5).astype(np.float32)
-    ln_w = rng.uniform(0.8, 1.2, D).astype(np.float32)
-    ln_b = rng.uniform(-0.1, 0.1, D).astype(np.float32)
-    bq = rng.uniform(-0.05, 0.05, D).astype(np.float32)
-    # raw Q4_0 blocks (ggml: f16 scale, 16 bytes; low nibble = element i, high = i + 16)
-    scales = rng.uniform(0.005, 0.02, (D, D // 32)).astype(np.float16)
-    nib = rng.integers(0, 16, (D, D // 32, 32), dtype=np.uint8)
-    raw = np.empty((D, D // 32, 18), dtype=np.uint8)
-    raw[:, :, :2] = scales.view(np.uint8).reshape(D, D // 32, 2)
-    raw[:, :, 2:] = nib[:, :, :16] | (nib[:, :, 16:] << 4)
-    w = (scales.astype(np.float64)[:, :, None] * (nib.astype(np.float64) - 8.0)).reshape(D, D)
-    k = rng.standard_normal((B, H, T, 64)).astype(np.float32)
-    v = rng.standard_normal((B, H, T, 64)).astype(np.float32)
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
-    got = whisper_amd.xattn_kv_fused_check(t(x), t(ln_w), t(ln_b), t(raw.reshape(-1)), t(bq), t(k), t(v),
-                                           Tq).cpu().numpy()
-    x64 = x.astype(np.float64)
-    mu = x64.mean(axis=1, keepdims=True)
-    ln = (x64 - mu) / np.sqrt(((x64 - mu) ** 2).mean(axis=1, keepdims=True) + 1e-5) * ln_w + ln_b
-    q = ln @ w.T + bq
-    qh = q.reshape(B, Tq, H, 64)
-    s = np.einsum("bqhd,bhtd->bhqt", qh, k.astype(np.float64)) / 8.0
-    s -= s.max(axis=-1, keepdims=True)
-    p = np.exp(s)
-    p /= p.sum(axis=-1, keepdims=True)
-    ref = np.einsum("bhqt,bhtd->bqhd", p, v.astype(np.float64)).reshape(B * Tq, D)
-    # f32 LayerNorm and D-term f32 dot products for q (|q| ~ 2), then the
-    # same f32 attention as the unfused form
-    err = np.abs(got - ref).max() / np.abs(v).max()
-    assert err <= 2e-5, err

@@ -18,6 +18,7 @@
 
 #include "../wq4_device.hpp"
 #include "../wq4_lnmath.hpp"
+#include "wa_headproj.hpp"
 #include "wa_kernels.hpp"
 
 namespace wa {
@@ -413,12 +414,12 @@ __device__ __forceinline__ void attn_scan(const floatx4 (&qv)[TQ], int Tq, int k
   }
 }
 
-// Merge the 4 groups of each wave, then the 4 waves, in a fixed order.  Wave
+// Merge the 4 groups of each wave, then the NWV waves, in a fixed order.  Wave
 // t (< Tq) returns query t's (mn, ls, os = unnormalised o[lane]).
-template <int TQ>
+template <int TQ, int NWV>
 __device__ __forceinline__ void attn_merge(int Tq, int wave, int lane, float (&m)[TQ], float (&l)[TQ],
-                                           floatx4 (&o)[TQ], float (&wm)[4][TQ], float (&wl)[4][TQ],
-                                           float (&wo)[4][TQ][64], float& mn, float& ls, float& os) {
+                                           floatx4 (&o)[TQ], float (&wm)[NWV][TQ], float (&wl)[NWV][TQ],
+                                           float (&wo)[NWV][TQ][64], float& mn, float& ls, float& os) {
   const int sub = lane & 15, grp = lane >> 4;
 #pragma unroll
   for (int t = 0; t < TQ; ++t) {
@@ -452,124 +453,13 @@ __device__ __forceinline__ void attn_merge(int Tq, int wave, int lane, float (&m
   if (wave < Tq) {
     const int t = wave;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) mn = fmaxf(mn, wm[w][t]);
+    for (int w = 0; w < NWV; ++w) mn = fmaxf(mn, wm[w][t]);
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NWV; ++w) {
       const float a = wm[w][t] == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(wm[w][t] - mn);
       ls += wl[w][t] * a;
       os += wo[w][t][lane] * a;
     }
-  }
-}
-
-// ----------------------------- in-launch projections (few clips) --
-// A decode step of a few clips is a chain of launches; where an attention
-// workgroup owns whole heads it can form its own projection of them instead
-// of waiting for a GEMM launch: LN(x) of its clip's Tq rows (f32,
-// wq4_lnmath.hpp, layers.rs:12-32) and 64 output columns from the raw GGUF
-// Q4_0 rows (f32 dequantised weights, f32 sums: linear.rs:34-40 over
-// tensor.rs dequantisation).  Lane tid owns column tid >> 2 and block pairs
-// (tid & 3) + 4 i (36 B, dword aligned).
-constexpr int kXkvMaxD = 1280;  // LDS rows of LN(x); n_text_state <= 1280
-constexpr int kXkvPairs = 5;    // Q4 block pairs per lane: D / 64 / 4 <= 5
-
-// LN(x) of row r = wave into xs[wave] (f32), the wave's own rows only.
-template <int TQ>
-__device__ __forceinline__ void xkv_ln_rows(const float* x, const float* ln_w, const float* ln_b, int b, int Tq,
-                                            int D, int wave, int lane, float (*xs)[kXkvMaxD]) {
-  if (wave >= Tq) return;
-  const float* xr = x + (size_t)(b * Tq + wave) * D;
-  floatx4 v[wq4::kLnMaxV];
-#pragma unroll
-  for (int i = 0; i < wq4::kLnMaxV; ++i) {
-    const int k = lane * 4 + 256 * i;
-    v[i] = k < D ? *reinterpret_cast<const floatx4*>(xr + k) : floatx4{0.f, 0.f, 0.f, 0.f};
-  }
-  float mean, den;
-  wq4::ln_row_stats(v, D, lane, mean, den);
-#pragma unroll
-  for (int i = 0; i < wq4::kLnMaxV; ++i) {
-    const int k = lane * 4 + 256 * i;
-    if (k < D) {
-      const floatx4 g = *reinterpret_cast<const floatx4*>(ln_w + k);
-      const floatx4 bb = *reinterpret_cast<const floatx4*>(ln_b + k);
-      floatx4 y;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) y[e] = wq4::ln_apply(v[i][e], mean, den, g[e], bb[e]);
-      *reinterpret_cast<floatx4*>(&xs[wave][k]) = y;
-    }
-  }
-}
-
-// This lane's words of 64 raw Q4_0 rows starting at w64 (K = D); past the
-// row: clamped address (the dot gives those pairs a zero weight).
-__device__ __forceinline__ void q4_rows_load(const uint8_t* w64, int D, int tid, uint32_t (&w)[kXkvPairs][9]) {
-  const int c = tid >> 2, jp = tid & 3, npairs = D / 64;
-  const uint32_t* wrow = reinterpret_cast<const uint32_t*>(w64 + (size_t)c * (D / 32) * 18);
-#pragma unroll
-  for (int i = 0; i < kXkvPairs; ++i) {
-    const int p = min(jp + 4 * i, npairs - 1);
-#pragma unroll
-    for (int e = 0; e < 9; ++e) w[i][e] = __builtin_nontemporal_load(wrow + p * 9 + e);
-  }
-}
-
-// One Q4_0 block (16 nibble bytes in n[4], scale d) dotted with LN(x)[k0 ..
-// k0 + 31] of every query row: element i = low nibble of byte i, i + 16 = high.
-template <int TQ>
-__device__ __forceinline__ void xkv_block_dot(const uint32_t (&n)[4], float d, int k0, int Tq,
-                                              const float (*xs)[kXkvMaxD], float (&acc)[TQ]) {
-#pragma unroll
-  for (int t = 0; t < TQ; ++t) {
-    if (t < Tq) {
-      float s = acc[t];
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const floatx4 xl = *reinterpret_cast<const floatx4*>(&xs[t][k0 + 4 * w]);
-        const floatx4 xh = *reinterpret_cast<const floatx4*>(&xs[t][k0 + 16 + 4 * w]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t byte = (n[w] >> (8 * e)) & 0xffu;
-          s = fmaf(d * (float)((int)(byte & 15u) - 8), xl[e], s);
-          s = fmaf(d * (float)((int)(byte >> 4) - 8), xh[e], s);
-        }
-      }
-      acc[t] = s;
-    }
-  }
-}
-
-// Column (tid >> 2) of the 64 rows loaded by q4_rows_load, dotted with the
-// Tq rows of xs; every lane of the column's 4 returns the same sum (fixed
-// order: block pairs in order per lane, then lanes (0 + 1) + (2 + 3)).
-template <int TQ>
-__device__ __forceinline__ void q4_rows_dot(const uint32_t (&w)[kXkvPairs][9], int D, int tid, int Tq,
-                                            const float (*xs)[kXkvMaxD], float (&acc)[TQ]) {
-  const int jp = tid & 3, npairs = D / 64;
-#pragma unroll
-  for (int t = 0; t < TQ; ++t) acc[t] = 0.0f;
-#pragma unroll
-  for (int i = 0; i < kXkvPairs; ++i) {
-    const bool ok = jp + 4 * i < npairs;
-    const int kp0 = (jp + 4 * i) * 64;
-    // block 2p: scale = bytes 0-1, nibbles = bytes 2-17; block 2p + 1:
-    // scale = bytes 18-19, nibbles = bytes 20-35 (words 5-8)
-    const float d0 = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[i][0] & 0xffffu));
-    const float d1 = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[i][4] >> 16));
-    const uint32_t n0[4] = {__builtin_amdgcn_alignbit(w[i][1], w[i][0], 16),
-                            __builtin_amdgcn_alignbit(w[i][2], w[i][1], 16),
-                            __builtin_amdgcn_alignbit(w[i][3], w[i][2], 16),
-                            __builtin_amdgcn_alignbit(w[i][4], w[i][3], 16)};
-    const uint32_t n1[4] = {w[i][5], w[i][6], w[i][7], w[i][8]};
-    if (ok) {
-      xkv_block_dot<TQ>(n0, d0, kp0, Tq, xs, acc);
-      xkv_block_dot<TQ>(n1, d1, kp0 + 32, Tq, xs, acc);
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < TQ; ++t) {
-    acc[t] += __shfl_xor(acc[t], 1, 64);
-    acc[t] += __shfl_xor(acc[t], 2, 64);
   }
 }
 
@@ -580,16 +470,11 @@ __device__ __forceinline__ void q4_rows_dot(const uint32_t (&w)[kXkvPairs][9], i
 // appended there for later steps and read here straight from the qkv rows.
 constexpr int kMaxCtx = 448;
 
-// FUSE (few clips, Q4_0 weights): the workgroup forms its head's q, k, v
-// itself -- LN(x) of its clip's rows (attn_ln) and 3 x 64 columns of the raw
-// query / key / value rows (q4_rows_load / q4_rows_dot) -- instead of reading
-// the qkv GEMM's rows: one launch fewer per layer.  The new keys / values go
-// to the cache first and are read back from it after the barrier.
-template <int NS, int TQ, bool FUSE>
+template <int NS, int TQ>
 __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restrict__ qkv, float* __restrict__ ck,
                                                             float* __restrict__ cv, int Tq_, int H, int ctx,
                                                             const DecodeState* state, int kv_len_host,
-                                                            _Float16* __restrict__ tiled, SelfFuseQkv fz) {
+                                                            _Float16* __restrict__ tiled) {
   const int Tq = TQ == 1 ? 1 : Tq_;
   __shared__ float wm[4][TQ], wl[4][TQ];
   __shared__ float wo[4][TQ][64];
@@ -603,53 +488,19 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
   const float* kb = ck + hb + sub * 4;
   const float* vb = cv + hb + sub * 4;
   const float* newb = qkv + (size_t)b * Tq * 3 * D + D + head * 64 + sub * 4;
-  if constexpr (FUSE) {
-    __shared__ float xs[TQ][kXkvMaxD];
-    __shared__ float qs[TQ][64];
-    const size_t wofs = (size_t)head * 64 * (D / 32) * 18;
-    uint32_t w[3][kXkvPairs][9];
-    q4_rows_load(fz.wq + wofs, D, tid, w[0]);
-    q4_rows_load(fz.wk + wofs, D, tid, w[1]);
-    q4_rows_load(fz.wv + wofs, D, tid, w[2]);
-    xkv_ln_rows<TQ>(fz.x, fz.ln_w, fz.ln_b, b, Tq, D, wave, lane, xs);
-    __syncthreads();
-    const int c = tid >> 2;
-#pragma unroll
-    for (int P = 0; P < 3; ++P) {
-      float acc[TQ];
-      q4_rows_dot<TQ>(w[P], D, tid, Tq, xs, acc);
-      if ((tid & 3) == 0) {
-        const float bias = fz.bqkv[P * D + head * 64 + c];
-#pragma unroll
-        for (int t = 0; t < TQ; ++t) {
-          if (t < Tq) {  // append the new keys / values (decoder.rs:77-112 via Tensor::cat)
-            const float val = acc[t] + bias;
-            if (P == 0) qs[t][c] = val;
-            else (P == 1 ? ck : cv)[hb + (size_t)(kv_len + t) * 64 + c] = val;
-          }
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < TQ; ++t)
-      qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(&qs[t][sub * 4]) * kEaQScale : floatx4{0.f, 0.f, 0.f, 0.f};
-  } else {
-    // append the new keys / values (decoder.rs:77-112 via Tensor::cat)
-    if (tid < Tq * 16) {
-      const int t = tid >> 4, s4 = (tid & 15) * 4;
-      const float* src = qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + s4;
-      *reinterpret_cast<floatx4*>(ck + hb + (size_t)(kv_len + t) * 64 + s4) =
-          *reinterpret_cast<const floatx4*>(src + D);
-      *reinterpret_cast<floatx4*>(cv + hb + (size_t)(kv_len + t) * 64 + s4) =
-          *reinterpret_cast<const floatx4*>(src + 2 * D);
-    }
-#pragma unroll
-    for (int t = 0; t < TQ; ++t)
-      qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + sub * 4) *
-                           kEaQScale
-                     : floatx4{0.f, 0.f, 0.f, 0.f};
+  // append the new keys / values (decoder.rs:77-112 via Tensor::cat)
+  if (tid < Tq * 16) {
+    const int t = tid >> 4, s4 = (tid & 15) * 4;
+    const float* src = qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + s4;
+    *reinterpret_cast<floatx4*>(ck + hb + (size_t)(kv_len + t) * 64 + s4) = *reinterpret_cast<const floatx4*>(src + D);
+    *reinterpret_cast<floatx4*>(cv + hb + (size_t)(kv_len + t) * 64 + s4) =
+        *reinterpret_cast<const floatx4*>(src + 2 * D);
   }
+#pragma unroll
+  for (int t = 0; t < TQ; ++t)
+    qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(qkv + (size_t)(b * Tq + t) * 3 * D + head * 64 + sub * 4) *
+                         kEaQScale
+                   : floatx4{0.f, 0.f, 0.f, 0.f};
   const int nk = kv_len + Tq;
   const int per_wave = (nk + 3) / 4;
   const int k0 = min(nk, wave * per_wave), k1 = min(nk, k0 + per_wave);
@@ -658,7 +509,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
   attn_scan<TQ, 8>(
       qv, Tq, k0, k1, grp,
       [&](int j, const float*& kp, const float*& vp) {
-        if (FUSE || j < kv_len) {
+        if (j < kv_len) {
           kp = kb + (size_t)j * 64;
           vp = vb + (size_t)j * 64;
         } else {  // this step's own keys: not yet visible through the cache
@@ -668,7 +519,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
       },
       [&](int t, int j) { return j <= kv_len + t; }, m, l, o);
   float mn, ls, os;
-  attn_merge<TQ>(Tq, wave, lane, m, l, o, wm, wl, wo, mn, ls, os);
+  attn_merge<TQ, 4>(Tq, wave, lane, m, l, o, wm, wl, wo, mn, ls, os);
   if (wave < Tq) {
     const int t = wave;
     const float val = os / ls;
@@ -677,27 +528,130 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
   }
 }
 
+// s_waitcnt vmcnt(N), N a compile-time count (part of the instruction)
+template <int N>
+__device__ __forceinline__ void vmcnt_wait() {
+  static_assert(N == 0 || N == 16 || N == 24, "add the count");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+}
+
+// Decode step (Tq = 1) of a few-clip group, Q4_0 weights: the self-attention
+// with its head's q / k / v formed inside the launch (decoder.rs:77-112,
+// attention.rs:93-125) -- one launch where the qkv GEMM + attention took two.
+// Workgroup (head, clip), 8 waves: the head's 12 column subtiles of the fused
+// qkv weight (q: 4 head, k: D/16 + 4 head, v: 2 D/16 + 4 head) and the clip's
+// A-tiled row of the LayerNorm fold (attn_ln) come into LDS by LDS-DMA
+// (wa_headproj.hpp; 149 KiB at D = 1280, one workgroup per CU), the eight
+// waves form the 192 values exactly as the decode-step GEMM would
+// (bit for bit), k / v are appended to the cache, and the keys are scanned
+// exactly as dec_self_attn_kernel scans them (this step's key from LDS).
+template <int NS>
+__global__ __launch_bounds__(512) void dec_self_attn_fused_kernel(HeadProj p, float* __restrict__ ck,
+                                                                  float* __restrict__ cv, int H, int ctx,
+                                                                  const DecodeState* __restrict__ state,
+                                                                  _Float16* __restrict__ tiled) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ float wm[8][1], wl[8][1];
+  __shared__ float wo[8][1][64];
+  __shared__ __attribute__((aligned(16))) float qkv_s[3][64];
+  __shared__ float srow[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int head = blockIdx.x, b = blockIdx.y;
+  const int D = H * 64;
+  const int sub = lane & 15, grp = lane >> 4;
+  const int kv_len = state->kv_len;
+  const size_t hb = ((size_t)b * H + head) * ctx * 64;
+  auto sub_of = [&](int s) { return (s >> 2) * (D / 16) + 4 * head + (s & 3); };
+  (void)hp_issue<12>(p, sub_of, b, smem, wave, 8, lane);
+  vmcnt_wait<0>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (wave == 0) {
+    float mean, den;
+    hp_row_stats<12>(p, smem, lane, mean, den);
+    if (lane == 0) {
+      srow[0] = mean;
+      srow[1] = den;
+    }
+  }
+  hp_compute<12>(p, smem, wave, 8, lane);
+  __syncthreads();
+  if (tid < 192) {
+    const float y = hp_finish<12>(p, smem, tid, srow[0], srow[1]);
+    const int part = tid >> 6, d = tid & 63;
+    qkv_s[part][d] = y;
+    // append k, v (decoder.rs:77-112 via Tensor::cat); read back from LDS below
+    if (part == 1) ck[hb + (size_t)kv_len * 64 + d] = y;
+    if (part == 2) cv[hb + (size_t)kv_len * 64 + d] = y;
+  }
+  __syncthreads();
+  // the scan of dec_self_attn_kernel (4 waves' key ranges, 8 keys in flight,
+  // the same merge: waves 4 .. 7 get empty ranges and merge as zeros), this
+  // step's key / value taken from LDS where that kernel reads the qkv rows
+  floatx4 qv[1];
+  qv[0] = *reinterpret_cast<const floatx4*>(&qkv_s[0][sub * 4]) * kEaQScale;
+  const floatx4 knew = *reinterpret_cast<const floatx4*>(&qkv_s[1][sub * 4]);
+  const floatx4 vnew = *reinterpret_cast<const floatx4*>(&qkv_s[2][sub * 4]);
+  const float* kb = ck + hb + sub * 4;
+  const float* vb = cv + hb + sub * 4;
+  const int nk = kv_len + 1;
+  const int per_wave = (nk + 3) / 4;
+  const int k0 = min(nk, wave * per_wave), k1 = min(nk, k0 + per_wave);
+  constexpr int U = 8;
+  float m[1], l[1];
+  floatx4 o[1];
+  attn_init<1>(m, l, o);
+  for (int j0 = k0; j0 < k1; j0 += 4 * U) {
+    floatx4 kk[U], vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = max(0, min(j0 + 4 * u + grp, k1 - 1));
+      const int jc = max(0, min(j, kv_len - 1));  // cache rows only: loads never branch
+      const floatx4 kc = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(kb + (size_t)jc * 64));
+      const floatx4 vc = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(vb + (size_t)jc * 64));
+      kk[u] = j < kv_len ? kc : knew;
+      vv[u] = j < kv_len ? vc : vnew;
+    }
+    attn_update<1, U>(qv, 1, j0, k1, grp, [](int, int) { return true; }, kk, vv, m, l, o);
+  }
+  float mn, ls, os;
+  attn_merge<1, 8>(1, wave, lane, m, l, o, wm, wl, wo, mn, ls, os);
+  if (wave == 0) {
+    const float val = os / ls;
+    const float v1 = __shfl_down(val, 1, 64), v2 = __shfl_down(val, 2, 64), v3 = __shfl_down(val, 3, 64);
+    if ((lane & 3) == 0) atile_store4<NS>(tiled, b, head * 64 + lane, kbp_of(D), val, v1, v2, v3);
+  }
+}
+
 hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float* cache_v, int B, int Tq, int H,
                                          int ctx, const DecodeState* state, int kv_len_host, _Float16* tiled,
-                                         int ns, hipStream_t st, const SelfFuseQkv* fuse) {
+                                         int ns, hipStream_t st) {
   if (Tq > 4 || ctx > kMaxCtx) return hipErrorInvalidValue;
-  if (fuse && (H * 64 > kXkvMaxD || !fuse->x || !fuse->ln_w || !fuse->ln_b || !fuse->wq || !fuse->wk ||
-               !fuse->wv || !fuse->bqkv))
-    return hipErrorInvalidValue;
-  const SelfFuseQkv fz = fuse ? *fuse : SelfFuseQkv{};
   const dim3 grid(H, B), block(256);
-#define WA_SELF(NS_, TQ_, F_)                                                                                    \
-  hipLaunchKernelGGL((dec_self_attn_kernel<NS_, TQ_, F_>), grid, block, 0, st, qkv, cache_k, cache_v, Tq, H, ctx, \
-                     state, kv_len_host, tiled, fz)
-#define WA_SELF2(NS_, TQ_) \
-  if (fuse) WA_SELF(NS_, TQ_, true); else WA_SELF(NS_, TQ_, false)
+#define WA_SELF(NS_, TQ_)                                                                                     \
+  hipLaunchKernelGGL((dec_self_attn_kernel<NS_, TQ_>), grid, block, 0, st, qkv, cache_k, cache_v, Tq, H, ctx, \
+                     state, kv_len_host, tiled)
   if (ns == 2) {
-    if (Tq == 1) { WA_SELF2(2, 1); } else { WA_SELF2(2, 4); }
+    if (Tq == 1) { WA_SELF(2, 1); } else { WA_SELF(2, 4); }
   } else {
-    if (Tq == 1) { WA_SELF2(1, 1); } else { WA_SELF2(1, 4); }
+    if (Tq == 1) { WA_SELF(1, 1); } else { WA_SELF(1, 4); }
   }
-#undef WA_SELF2
 #undef WA_SELF
+  return hipGetLastError();
+}
+
+bool fused_proj_supported(int D, int ns) { return ns == 2 && hp_supported(12, D) && hp_supported(4, D); }
+
+hipError_t launch_decoder_self_attention_fused(const HeadProj& p, float* cache_k, float* cache_v, int B, int H, int ctx,
+                                               const DecodeState* state, _Float16* tiled, int ns, hipStream_t st) {
+  if (!state || ctx > kMaxCtx || H * 64 != p.K || !fused_proj_supported(p.K, ns) || !p.q16 || !p.d16 || !p.at ||
+      !p.stats || !p.wg || !p.b2 || p.ku * 128 != p.K)
+    return hipErrorInvalidValue;
+  const size_t lds = hp_lds_bytes(12, p.ku);
+  hipLaunchKernelGGL((dec_self_attn_fused_kernel<2>), dim3(H, B), dim3(512), lds, st, p, cache_k, cache_v, H, ctx,
+                     state, tiled);
   return hipGetLastError();
 }
 
@@ -720,31 +674,31 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
 constexpr int kXkvMaxSplit = 32;
 constexpr int kXkvPart = 68;  // floats per (query) partial: o[64], m, l, pad
 
+// 188 keys per split (8 splits at T = 1500, <= 47 keys per wave: one
+// 12-deep scan pass); measured at one clip (Large-V3, in the decode step):
+// 9.2 us per launch vs 9.9 at 96 keys, 11.1 at 375, 13.4 at 48 (r03).  A
+// function of T only: a clip's bits do not depend on its batch.
+constexpr int kXkvKeys = 188;
 int cross_attention_kv_splits(int T) {
-  static const int keys = [] {  // keys per split (A/B knob WA_XKV_KEYS; a function of T only either way)
-    const char* e = getenv("WA_XKV_KEYS");
-    const int v = e ? atoi(e) : 188;
-    return v >= 16 ? v : 188;
-  }();
-  // 188 (8 splits at T = 1500, <= 47 keys per wave: one 12-deep scan pass);
-  // measured at one clip (Large-V3, in the decode step): 9.2 us per launch
-  // vs 9.9 at 96 keys, 11.1 at 375, 13.4 at 48
-  const int s = (T + keys - 1) / keys;
+  const int s = (T + kXkvKeys - 1) / kXkvKeys;
   return s < 1 ? 1 : (s > kXkvMaxSplit ? kXkvMaxSplit : s);
 }
 
-// FUSEQ: the query projection runs inside the kernel (one clip's decode
-// step is a chain of launches, and this removes one): each workgroup forms
-// LN(x) of its clip's Tq rows (cross_attn_ln) and q of its head's 64 columns
-// (q4_rows_load / q4_rows_dot above) while the first pass of K / V loads is
-// already in flight.
+// FUSEQ (decode steps, Tq = 1, Q4_0 weights): the query projection runs
+// inside the launch -- the cq GEMM launch of the chain disappears.  Each
+// workgroup brings its head's 4 column subtiles of Wq (decode-step layout),
+// the clip's A-tiled cross_attn_ln fold row and the fold vectors into LDS by
+// LDS-DMA, issues its first pass of K / V loads behind them, and forms q of
+// its head with the decode-step GEMM's arithmetic (wa_headproj.hpp: the same
+// bits as that GEMM launch) while those loads fly.
 template <int NS, int TQ, bool FUSEQ>
 __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restrict__ q, const float* __restrict__ kc,
                                                             const float* __restrict__ vc, int Tq_, int T, int H,
                                                             int S, float* __restrict__ part,
                                                             int* __restrict__ counters,
-                                                            _Float16* __restrict__ tiled, XkvFuseQ fq) {
+                                                            _Float16* __restrict__ tiled, HeadProj fq) {
   constexpr int U = TQ == 1 ? 12 : 8;  // <= 48 keys per wave in flight at once (decode step)
+  static_assert(!FUSEQ || TQ == 1, "the fused query is a decode-step form");
   const int Tq = TQ == 1 ? 1 : Tq_;
   __shared__ float wm[4][TQ], wl[4][TQ];
   __shared__ float wo[4][TQ][64];
@@ -770,24 +724,30 @@ __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restr
   attn_init<TQ>(m, l, o);
   int j0 = k0;
   if constexpr (FUSEQ) {
-    __shared__ float xs[TQ][kXkvMaxD];
-    __shared__ float qs[TQ][64];
-    const int c = tid >> 2;
-    uint32_t w[kXkvPairs][9];
-    q4_rows_load(fq.wq + (size_t)head * 64 * (D / 32) * 18, D, tid, w);
-    floatx4 kk[U], vv[U];  // the first pass of K / V, before q exists
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ float qs[64];
+    __shared__ float srow[2];
+    (void)hp_issue<4>(fq, [&](int s) { return 4 * head + s; }, b, smem, wave, 4, lane);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    floatx4 kk[U], vv[U];  // the first pass of K / V, in flight behind the LDS-DMA
     attn_fetch<U>(j0, k1, grp, rows, kk, vv);
-    xkv_ln_rows<TQ>(fq.x, fq.ln_w, fq.ln_b, b, Tq, D, wave, lane, xs);
+    vmcnt_wait<2 * U>();   // every DMA piece has landed; the 2U younger K / V loads may still fly
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (wave == 0) {
+      float mean, den;
+      hp_row_stats<4>(fq, smem, lane, mean, den);
+      if (lane == 0) {
+        srow[0] = mean;
+        srow[1] = den;
+      }
+    }
+    hp_compute<4>(fq, smem, wave, 4, lane);
     __syncthreads();
-    float acc[TQ];
-    q4_rows_dot<TQ>(w, D, tid, Tq, xs, acc);
-#pragma unroll
-    for (int t = 0; t < TQ; ++t)
-      if ((tid & 3) == 0 && t < Tq) qs[t][c] = acc[t] + fq.bq[head * 64 + c];
+    if (tid < 64) qs[tid] = hp_finish<4>(fq, smem, tid, srow[0], srow[1]);
     __syncthreads();
-#pragma unroll
-    for (int t = 0; t < TQ; ++t)
-      qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(&qs[t][sub * 4]) * kEaQScale : floatx4{0.f, 0.f, 0.f, 0.f};
+    qv[0] = *reinterpret_cast<const floatx4*>(&qs[sub * 4]) * kEaQScale;
     if (j0 < k1) attn_update<TQ, U>(qv, Tq, j0, k1, grp, [](int, int) { return true; }, kk, vv, m, l, o);
     j0 += 4 * U;
   } else {
@@ -803,7 +763,7 @@ __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restr
     attn_update<TQ, U>(qv, Tq, j0, k1, grp, [](int, int) { return true; }, kk, vv, m, l, o);
   }
   float mn, ls, os;
-  attn_merge<TQ>(Tq, wave, lane, m, l, o, wm, wl, wo, mn, ls, os);
+  attn_merge<TQ, 4>(Tq, wave, lane, m, l, o, wm, wl, wo, mn, ls, os);
   if (S > 1) {
     typedef __attribute__((address_space(1))) float gfloat;
     typedef __attribute__((address_space(1))) int gint;
@@ -864,25 +824,25 @@ size_t cross_attention_kv_part_floats(int B, int H, int T) {
 
 hipError_t launch_cross_attention_kv(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
                                      float* part, int* counters, _Float16* tiled, int ns, hipStream_t st,
-                                     const XkvFuseQ* fuse) {
+                                     const HeadProj* fuse) {
   if (Tq < 1 || Tq > 4 || B < 1 || T < 1 || H < 1) return hipErrorInvalidValue;
-  if (fuse && (H * 64 > kXkvMaxD || (H * 64) / 64 > 4 * kXkvPairs || !fuse->x || !fuse->ln_w || !fuse->ln_b ||
-               !fuse->wq || !fuse->bq))
+  if (fuse && (Tq != 1 || H * 64 != fuse->K || !fused_proj_supported(fuse->K, ns) || fuse->ku * 128 != fuse->K ||
+               !fuse->q16 || !fuse->d16 || !fuse->at || !fuse->stats || !fuse->wg || !fuse->b2))
     return hipErrorInvalidValue;
-  const XkvFuseQ fq = fuse ? *fuse : XkvFuseQ{};
+  if (!fuse && !q) return hipErrorInvalidValue;
+  const HeadProj fq = fuse ? *fuse : HeadProj{};
   const int S = cross_attention_kv_splits(T);
   const dim3 grid(H * S, B), block(256);
-#define WA_XKV(NS_, TQ_, F_)                                                                                 \
-  hipLaunchKernelGGL((cross_attn_kv_kernel<NS_, TQ_, F_>), grid, block, 0, st, q, k, v, Tq, T, H, S, part, \
+#define WA_XKV(NS_, TQ_, F_, LDS_)                                                                              \
+  hipLaunchKernelGGL((cross_attn_kv_kernel<NS_, TQ_, F_>), grid, block, LDS_, st, q, k, v, Tq, T, H, S, part, \
                      counters, tiled, fq)
-#define WA_XKV2(NS_, TQ_) \
-  if (fuse) WA_XKV(NS_, TQ_, true); else WA_XKV(NS_, TQ_, false)
-  if (ns == 2) {
-    if (Tq == 1) { WA_XKV2(2, 1); } else { WA_XKV2(2, 4); }
+  if (fuse) {
+    WA_XKV(2, 1, true, (size_t)hp_lds_bytes(4, fuse->ku));
+  } else if (ns == 2) {
+    if (Tq == 1) { WA_XKV(2, 1, false, 0); } else { WA_XKV(2, 4, false, 0); }
   } else {
-    if (Tq == 1) { WA_XKV2(1, 1); } else { WA_XKV2(1, 4); }
+    if (Tq == 1) { WA_XKV(1, 1, false, 0); } else { WA_XKV(1, 4, false, 0); }
   }
-#undef WA_XKV2
 #undef WA_XKV
   return hipGetLastError();
 }

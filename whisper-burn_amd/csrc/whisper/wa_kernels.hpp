@@ -26,22 +26,29 @@ hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Floa
 // appends k, v of the Tq new tokens at cache index kv_len (+ kv_base_extra)
 // and attends over kv_len + Tq entries, causal inside the new tokens when
 // Tq > 1 (attention.rs:270-287).  cache_k/v: [B, ctx, D].
-// With fuse != nullptr (few clips, Q4_0) qkv is not read: each workgroup
-// forms its head's q, k, v from LN(x) (attn_ln) and the raw Q4_0 query / key
-// / value rows [D][D / 32][18 B], bias bqkv [3D] (key part 0).
-struct SelfFuseQkv {
-  const float* x;
-  const float* ln_w;
-  const float* ln_b;
-  const uint8_t* wq;
-  const uint8_t* wk;
-  const uint8_t* wv;
-  const float* bqkv;
-};
 hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float* cache_v, int B, int Tq, int H,
                                          int ctx, const DecodeState* state, int kv_len_host, _Float16* tiled,
-                                         int ns, hipStream_t st,
-                                         const SelfFuseQkv* fuse = nullptr);
+                                         int ns, hipStream_t st);
+
+// In-launch projections of a few-clip decode step (wa_headproj.hpp): the
+// projection's decode-step weight layout + the LayerNorm-fold operand it
+// reads.  Supported for f16x2 operands (ns == 2), D % 256 == 0, D <= 1280.
+struct HeadProj {
+  const uint32_t* q16;  // decode-step nibbles of the weight (wq4_tensor_decode_layout)
+  const uint16_t* d16;  //   its f16 block scales
+  int ku;               // units of 4 Q4 blocks per 16-column subtile (K / 128)
+  const _Float16* at;   // A-tiled f16-pair operand of the rows: the LayerNorm-fold x * gamma (m-tile 0)
+  const float* stats;   // the fold producer's (mean, M2) per (row, 16-column tile) [rows][K / 16][2]
+  const float* wg;      // W gamma [N]
+  const float* b2;      // W beta + bias [N]
+  int K;                // input width (= n_text_state)
+};
+bool fused_proj_supported(int D, int ns);
+// The decode step's (Tq = 1) self-attention with its head's q / k / v formed
+// in the launch from the fused qkv weight (p: N = 3D, the attn_ln fold) --
+// the qkv GEMM launch and this attention in one launch, the same bits.
+hipError_t launch_decoder_self_attention_fused(const HeadProj& p, float* cache_k, float* cache_v, int B, int H, int ctx,
+                                               const DecodeState* state, _Float16* tiled, int ns, hipStream_t st);
 
 // Cross-attention over cached K / V (attention.rs:177-236, the reference's
 // form; used for decode groups of a few clips): q [B*Tq, D] f32, k / v
@@ -49,20 +56,14 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
 // output), Tq <= 4; part: cross_attention_kv_part_floats floats, counters:
 // B * H ints zeroed once (re-armed by the kernel).  Writes the A-tiled
 // operand of the output projection.
-// With fuse != nullptr q is not read: the kernel forms it from the residual
-// rows x [B*Tq, D] (q = LN(x) Wq^T + bq, Wq as raw Q4_0 rows, D <= 1280).
-struct XkvFuseQ {
-  const float* x;
-  const float* ln_w;
-  const float* ln_b;
-  const uint8_t* wq;
-  const float* bq;
-};
+// With fuse != nullptr (Tq = 1) q is not read: each workgroup forms its
+// head's query from the cq weight (the cross_attn_ln fold, wa_headproj.hpp),
+// the same bits as the cq GEMM launch it replaces.
 int cross_attention_kv_splits(int T);
 size_t cross_attention_kv_part_floats(int B, int H, int T);
 hipError_t launch_cross_attention_kv(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
                                      float* part, int* counters, _Float16* tiled, int ns, hipStream_t st,
-                                     const XkvFuseQ* fuse = nullptr);
+                                     const HeadProj* fuse = nullptr);
 
 // Cross-attention over the encoder output (wa_xattn.hip; attention.rs:
 // 204-298 restated without K/V caches): q [B*Tq, D] f32 (rows b*Tq + i),

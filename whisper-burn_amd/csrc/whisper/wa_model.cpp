@@ -155,8 +155,11 @@ struct DecLayer {
   // cross-attention key / value weights in raw GGUF form (Q4_0 blocks or
   // f16), read by the K/V-cache-free cross-attention (wa_xattn.hip)
   uint8_t *ck_raw = nullptr, *cv_raw = nullptr;
-  uint8_t* cq_raw = nullptr;
-  uint8_t *sq_raw = nullptr, *sk_raw = nullptr, *sv_raw = nullptr;  // raw Q4_0 self q / k / v rows (few clips)  // raw Q4_0 query rows: the fused q of the K / V cross-attention (few clips)
+  // decode-step layouts of qkv and cq (wq4_tensor_decode_layout) for the
+  // in-launch projections of few-clip decode steps (wa_headproj.hpp)
+  const uint32_t *qkv_q16 = nullptr, *cq_q16 = nullptr;
+  const uint16_t *qkv_d16 = nullptr, *cq_d16 = nullptr;
+  int64_t proj_ku = 0;
   uint32_t* cv_p = nullptr;  // Q4_0: cv_raw in the projection's lane order (wa::launch_wv_pack)
   float *cache_k, *cache_v;
   // few-clip decode groups (wa_model::kv_clips): the reference's per-layer
@@ -243,6 +246,10 @@ struct wa_model {
   // |beta|); still flagged -> WQ4_ERANGE, never NaN tokens.
   int* range_flag = nullptr;
   bool wide_range = false;
+  // few-clip decode steps form the qkv / cq projections inside the attention
+  // launches (wa_headproj.hpp); off only for the bit-equality test
+  // (wa_model_set_fused_projections)
+  bool fuse_proj = true;
   float timings[5] = {0, 0, 0, 0, 0};
   // decode-step logit trace (wa_transcribe_trace; null otherwise): device
   // [clip][trace_s1][trace_k] ids and their logits
@@ -392,27 +399,6 @@ struct GgufSource : Source {
   }
 };
 
-// A/B knobs, off by default (measured slower):
-// WA_XKV_FUSEQ=1 lets the K / V cross-attention form its own query
-// (cross_attn_ln + the query projection inside the launch) and
-// WA_SELF_FUSE=1 the decoder self-attention its own q / k / v, instead of the
-// LayerNorm-fold GEMMs; same tokens either way.
-bool kv_fuse_q() {
-  static const bool on = [] {
-    const char* e = getenv("WA_XKV_FUSEQ");
-    return e && atoi(e) != 0;
-  }();
-  return on;
-}
-
-bool self_fuse() {
-  static const bool on = [] {
-    const char* e = getenv("WA_SELF_FUSE");
-    return e && atoi(e) != 0;
-  }();
-  return on;
-}
-
 struct Builder {
   wa_model* m;
   Source& src;
@@ -560,19 +546,12 @@ wq4_status build_model(wa_model* m, Source& src) {
     L.ln1_b = B.vec(p + ".attn_ln.bias", Dt, -0.05f, 0.05f);
     L.qkv = B.q4({p + ".attn.query.weight", p + ".attn.key.weight", p + ".attn.value.weight"}, {Dt, Dt, Dt}, Dt);
     L.qkv_b = B.bias_cat({p + ".attn.query.bias", p + ".attn.key.bias", p + ".attn.value.bias"}, Dt);
-    if (m->kv_clips > 0 && m->wtype == 0 && self_fuse() && Dt <= 1280) {  // the fused self-attention's q / k / v
-      L.sq_raw = B.raw(p + ".attn.query.weight", Dt, Dt);
-      L.sk_raw = B.raw(p + ".attn.key.weight", Dt, Dt);
-      L.sv_raw = B.raw(p + ".attn.value.weight", Dt, Dt);
-    }
     L.out = B.q4({p + ".attn.out.weight"}, {Dt}, Dt);
     L.out_b = B.vec(p + ".attn.out.bias", Dt, -0.02f, 0.02f);
     L.ln2_w = B.vec(p + ".cross_attn_ln.weight", Dt, 0.9f, 1.1f);
     L.ln2_b = B.vec(p + ".cross_attn_ln.bias", Dt, -0.05f, 0.05f);
     L.cq = B.q4({p + ".cross_attn.query.weight"}, {Dt}, Dt);
     L.cq_b = B.vec(p + ".cross_attn.query.bias", Dt, -0.02f, 0.02f);
-    if (m->kv_clips > 0 && m->wtype == 0 && kv_fuse_q() && Dt <= 1280)  // the K / V cross-attention's own q
-      L.cq_raw = B.raw(p + ".cross_attn.query.weight", Dt, Dt);
     // cross-attention key / value (loader.rs:205-210; the key bias, absent
     // in Whisper, cancels in the softmax and is not needed)
     L.ck_raw = B.raw(p + ".cross_attn.key.weight", Dt, D);
@@ -598,6 +577,12 @@ wq4_status build_model(wa_model* m, Source& src) {
     L.fc2 = B.q4({p + ".mlp.2.weight"}, {Dt}, Ft);
     L.fc2_b = B.vec(p + ".mlp.2.bias", Dt, -0.02f, 0.02f);
     if (B.st != WQ4_OK) return B.st;
+    if (m->wtype == 0) {  // Q4_0: the few-clip decode step's in-launch projections read these
+      int64_t ku2 = 0;
+      if (wq4_tensor_decode_layout(L.qkv, &L.qkv_q16, &L.qkv_d16, &L.proj_ku) != WQ4_OK ||
+          wq4_tensor_decode_layout(L.cq, &L.cq_q16, &L.cq_d16, &ku2) != WQ4_OK || ku2 != L.proj_ku)
+        L.qkv_q16 = L.cq_q16 = nullptr;
+    }
   }
   m->dln_w = B.vec("decoder.ln.weight", Dt, 0.9f, 1.1f);
   m->dln_b = B.vec("decoder.ln.bias", Dt, -0.05f, 0.05f);
@@ -913,34 +898,36 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
   const int nl = (int)m->dec.size();
   for (int li = 0; li < nl; ++li) {  // DecoderBlock (decoder.rs:77-112 / 140-183)
     DecLayer& L = m->dec[li];
-    // few clips with Q4_0 weights: attn_ln and the q / k / v projections run
-    // inside the self-attention launch (SelfFuseQkv), from the residual rows
-    const bool fuse_sa = m->group_kv(g) && L.sq_raw != nullptr;
-    if (fuse_sa) {
-    } else if (fold) {
-      const wq4_ln_fold cons1{nullptr, nullptr, nullptr, g.ln_stats, L.qkv_wg};
-      WA_WQ4(wq4_gemm_tiled_lnfold(L.qkv, L.qkv_b2, g.atd_ln, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, &cons1,
-                                   st));
+    // few-clip decode steps (Q4_0, f16x2): the self-attention forms its head's
+    // q / k / v and the K / V cross-attention its query inside their own
+    // launches from the LayerNorm-fold operand (wa_headproj.hpp) -- the qkv
+    // and cq GEMM launches leave the chain, the values are the same bits
+    const bool fuse = fold && m->fuse_proj && m->group_kv(g) && L.qkv_q16 != nullptr && L.cq_q16 != nullptr &&
+                      wa::fused_proj_supported(D, m->ns);
+    if (fuse) {
+      const wa::HeadProj hp{L.qkv_q16, L.qkv_d16, (int)L.proj_ku, g.atd_ln, g.ln_stats, L.qkv_wg, L.qkv_b2, D};
+      WA_HIP(wa::launch_decoder_self_attention_fused(hp, L.cache_k + self_ofs, L.cache_v + self_ofs, B, H,
+                                                     c.n_text_ctx, state, g.atd_dec, m->ns, st));
     } else {
-      WA_WQ4(wq4_layernorm(g.xd, L.ln1_w, L.ln1_b, rows, D, m->prec, g.atd_dec, nullptr, st));
-      WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, g.atd_dec, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, 2, st));
+      if (fold) {
+        const wq4_ln_fold cons1{nullptr, nullptr, nullptr, g.ln_stats, L.qkv_wg};
+        WA_WQ4(wq4_gemm_tiled_lnfold(L.qkv, L.qkv_b2, g.atd_ln, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, &cons1,
+                                     st));
+      } else {
+        WA_WQ4(wq4_layernorm(g.xd, L.ln1_w, L.ln1_b, rows, D, m->prec, g.atd_dec, nullptr, st));
+        WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, g.atd_dec, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, 2, st));
+      }
+      WA_HIP(wa::launch_decoder_self_attention(g.qkvd, L.cache_k + self_ofs, L.cache_v + self_ofs, B, Tq, H,
+                                               c.n_text_ctx, state, kv0, g.atd_dec, m->ns, st));
     }
-    const wa::SelfFuseQkv fz{g.xd, L.ln1_w, L.ln1_b, L.sq_raw, L.sk_raw, L.sv_raw, L.qkv_b};
-    WA_HIP(wa::launch_decoder_self_attention(g.qkvd, L.cache_k + self_ofs, L.cache_v + self_ofs, B, Tq, H,
-                                             c.n_text_ctx, state, kv0, g.atd_dec, m->ns, st,
-                                             fuse_sa ? &fz : nullptr));
-    // few clips with Q4_0 weights: cross_attn_ln and the query projection
-    // run inside the K / V cross-attention launch (launch_cross_attention_kv
-    // with XkvFuseQ), which reads the residual rows directly
-    const bool fuse_q = m->group_kv(g) && L.cq_raw != nullptr;
-    if (fuse_q) {
-      WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
-    } else if (fold) {
+    if (fold) {
       const wq4_ln_fold prod2{L.ln2_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
       WA_WQ4(wq4_gemm_tiled_lnfold(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec,
                                    &prod2, st));
-      const wq4_ln_fold cons2{nullptr, nullptr, nullptr, g.ln_stats, L.cq_wg};
-      WA_WQ4(wq4_gemm_tiled_lnfold(L.cq, L.cq_b2, g.atd_ln, nullptr, g.qd, nullptr, rows, 0u, m->prec, &cons2, st));
+      if (!fuse) {
+        const wq4_ln_fold cons2{nullptr, nullptr, nullptr, g.ln_stats, L.cq_wg};
+        WA_WQ4(wq4_gemm_tiled_lnfold(L.cq, L.cq_b2, g.atd_ln, nullptr, g.qd, nullptr, rows, 0u, m->prec, &cons2, st));
+      }
     } else {
       WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
       WA_WQ4(wq4_layernorm(g.xd, L.ln2_w, L.ln2_b, rows, D, m->prec, g.atd_dec, nullptr, st));
@@ -948,9 +935,9 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
     }
     if (m->group_kv(g)) {  // few clips: one GEMV launch over the cached K / V
       const size_t kofs = (size_t)g.b0 * T * D;
-      const wa::XkvFuseQ fq{g.xd, L.ln2_w, L.ln2_b, L.cq_raw, L.cq_b};
-      WA_HIP(wa::launch_cross_attention_kv(g.qd, L.xk + kofs, L.xv + kofs, B, Tq, T, H, g.xkv_part, g.xkv_ctr,
-                                           g.atd_dec, m->ns, st, fuse_q ? &fq : nullptr));
+      const wa::HeadProj hq{L.cq_q16, L.cq_d16, (int)L.proj_ku, g.atd_ln, g.ln_stats, L.cq_wg, L.cq_b2, D};
+      WA_HIP(wa::launch_cross_attention_kv(fuse ? nullptr : g.qd, L.xk + kofs, L.xv + kofs, B, Tq, T, H, g.xkv_part,
+                                           g.xkv_ctr, g.atd_dec, m->ns, st, fuse ? &hq : nullptr));
     } else {
       WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, Tq, T, H, D, g.xqt,
                               g.xattn_part, g.atd_dec, m->ns, st));
@@ -963,7 +950,7 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
       WA_WQ4(wq4_gemm_tiled_lnfold(L.fc1, L.fc1_b2, g.atd_ln, nullptr, nullptr, g.atf_dec, rows,
                                    WQ4_EPI_GELU | WQ4_EPI_TILED_OUT, m->prec, &cons3, st));
       // the next layer's attn_ln (none after the last layer: decoder.ln below)
-      const bool nxt = li + 1 < nl && !fuse_sa;  // a fused self-attention forms its own attn_ln
+      const bool nxt = li + 1 < nl;
       const wq4_ln_fold prod1{nxt ? m->dec[li + 1].ln1_w : nullptr, nxt ? g.atd_ln : nullptr,
                               nxt ? g.ln_stats : nullptr, nullptr, nullptr};
       WA_WQ4(wq4_gemm_tiled_lnfold(L.fc2, L.fc2_b, g.atf_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec,
@@ -1067,7 +1054,7 @@ wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
   // encoder-plane offsets), the EOT mode and the trace buffers
   const int64_t key =
       (((((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0)) * 2 +
-       (m->group_kv(g) ? 1 : 0)) * 2 + (m->wide_range ? 1 : 0);
+       (m->group_kv(g) ? 1 : 0)) * 4 + (m->wide_range ? 1 : 0) + (m->fuse_proj ? 2 : 0);
   if (g.graph && g.graph_key == key) return WQ4_OK;
   if (g.graph) {
     (void)hipGraphExecDestroy(g.graph);
@@ -1491,6 +1478,13 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
 
 int wa_model_wide_range(const wa_model* m) { return m ? (m->wide_range ? 1 : 0) : -1; }
 
+int wa_model_set_fused_projections(wa_model* m, int on) {
+  if (!m) return -1;
+  const int prev = m->fuse_proj ? 1 : 0;
+  m->fuse_proj = on != 0;
+  return prev;
+}
+
 wq4_status wa_transcribe_trace(wa_model* m, const float* mel_dev, int n_clips, int lang_token, int max_tokens,
                                int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out, const int32_t* trace_ids_dev,
                                int trace_k, float* trace_out_dev, void* stream) {
@@ -1623,29 +1617,6 @@ wq4_status wa_xattn_kv_check(int device, const float* q_dev, const float* k_dev,
   WA_HIP(hipMemset(ctr, 0, (size_t)n_clips * H * sizeof(int)));
   WA_HIP(hipMemset(tiled, 0, tb));
   WA_HIP(wa::launch_cross_attention_kv(q_dev, k_dev, v_dev, n_clips, Tq, T, H, part, ctr, tiled, ns, nullptr));
-  WA_HIP(wa::launch_untile(tiled, R, D, ns, out_dev, nullptr));
-  WA_HIP(hipDeviceSynchronize());
-  return WQ4_OK;
-}
-
-wq4_status wa_xattn_kv_fused_check(int device, const float* x_dev, const float* ln_w_dev, const float* ln_b_dev,
-                                   const uint8_t* wq_dev, const float* bq_dev, const float* k_dev, const float* v_dev,
-                                   int n_clips, int Tq, int T, int H, wq4_precision prec, float* out_dev) {
-  if (!x_dev || !ln_w_dev || !ln_b_dev || !wq_dev || !bq_dev || !k_dev || !v_dev || !out_dev)
-    return fail(WQ4_EINVAL, "null argument");
-  if (n_clips < 1 || Tq < 1 || Tq > 4 || T < 1 || H < 1 || H > 20 || H % 2) return fail(WQ4_EINVAL, "bad sizes");
-  const int D = 64 * H, ns = prec == WQ4_PREC_F16 ? 1 : 2, R = n_clips * Tq;
-  WA_HIP(hipSetDevice(device));
-  Dev d;
-  auto* part = d.alloc<float>(wa::cross_attention_kv_part_floats(n_clips, H, T));
-  auto* ctr = d.alloc<int>((size_t)n_clips * H);
-  const size_t tb = wq4_atiled_bytes(R, D, prec);
-  auto* tiled = d.alloc<_Float16>(tb / 2);
-  if (!part || !ctr || !tiled) return fail(WQ4_ENOMEM, "allocation failed");
-  WA_HIP(hipMemset(ctr, 0, (size_t)n_clips * H * sizeof(int)));
-  WA_HIP(hipMemset(tiled, 0, tb));
-  const wa::XkvFuseQ fq{x_dev, ln_w_dev, ln_b_dev, wq_dev, bq_dev};
-  WA_HIP(wa::launch_cross_attention_kv(nullptr, k_dev, v_dev, n_clips, Tq, T, H, part, ctr, tiled, ns, nullptr, &fq));
   WA_HIP(wa::launch_untile(tiled, R, D, ns, out_dev, nullptr));
   WA_HIP(hipDeviceSynchronize());
   return WQ4_OK;

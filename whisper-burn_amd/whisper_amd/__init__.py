@@ -55,6 +55,8 @@ def lib() -> ctypes.CDLL:
         L.wa_model_weight_type.restype = c_int
         L.wa_model_wide_range.argtypes = [vp]
         L.wa_model_wide_range.restype = c_int
+        L.wa_model_set_fused_projections.argtypes = [vp, c_int]
+        L.wa_model_set_fused_projections.restype = c_int
         L.wa_model_create_from_gguf.argtypes = [c_int, ctypes.c_char_p, c_int, c_int, c_int, ctypes.POINTER(vp)]
         L.wa_gguf_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
         L.wa_gguf_close.argtypes = [vp]
@@ -71,13 +73,11 @@ def lib() -> ctypes.CDLL:
         L.wa_mel_filterbank.argtypes = [c_int, f32p, f32p]
         L.wa_xattn_check.argtypes = [c_int, vp, vp, vp, vp, c_int, vp, c_int, c_int, c_int, c_int, c_int, vp]
         L.wa_xattn_kv_check.argtypes = [c_int, vp, vp, vp, c_int, c_int, c_int, c_int, c_int, vp]
-        L.wa_xattn_kv_fused_check.argtypes = [c_int, vp, vp, vp, vp, vp, vp, vp, c_int, c_int, c_int, c_int, c_int,
-                                              vp]
         L.wa_transcribe_trace.argtypes = [vp, vp, c_int, c_int, c_int, c_int, i32p, i32p, vp, c_int, vp, vp]
         L.wa_encoder_attention_check.argtypes = [c_int, vp, c_int, c_int, c_int, c_int, vp]
         L.wa_self_attention_check.argtypes = [c_int, vp, vp, vp, c_int, c_int, c_int, c_int, c_int, c_int, vp]
         L.wa_logits_argmax_check.argtypes = [c_int, vp, vp, c_int, c_int, c_int, c_int, c_int, vp, vp]
-        for n in ("wa_xattn_check", "wa_xattn_kv_check", "wa_xattn_kv_fused_check", "wa_transcribe_trace", "wa_encoder_attention_check", "wa_self_attention_check",
+        for n in ("wa_xattn_check", "wa_xattn_kv_check", "wa_transcribe_trace", "wa_encoder_attention_check", "wa_self_attention_check",
                   "wa_logits_argmax_check", "wa_log_mel", "wa_mel_filterbank", "wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
                   "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read", "wa_probe_kernels",
                   "wa_decode_group_rows",
@@ -169,21 +169,6 @@ def xattn_kv_check(q, k, v, Tq: int, precision: int = wq4.PREC_F16X2):
     dev = k.device.index if k.device.index is not None else 0
     ptr = lambda t: ctypes.c_void_p(t.contiguous().data_ptr())
     check(lib().wa_xattn_kv_check(dev, ptr(q), ptr(k), ptr(v), B, Tq, T, H, precision, ptr(out)))
-    return out
-
-
-def xattn_kv_fused_check(x, ln_w, ln_b, wq_raw, bq, k, v, Tq: int, precision: int = wq4.PREC_F16X2):
-    """The K / V cross-attention with its query projection inside the launch
-    (wa_xattn_kv_fused_check): x cuda f32 [B*Tq, 64H] residual rows, ln_w /
-    ln_b / bq cuda f32 [64H], wq_raw cuda uint8 raw Q4_0 rows of Wq, k / v
-    cuda f32 head-major [B, H, T, 64] -> [B*Tq, 64H]."""
-    torch = _torch()
-    B, H, T, _ = k.shape
-    out = torch.empty((B * Tq, 64 * H), device=k.device, dtype=torch.float32)
-    dev = k.device.index if k.device.index is not None else 0
-    ptr = lambda t: ctypes.c_void_p(t.contiguous().data_ptr())
-    check(lib().wa_xattn_kv_fused_check(dev, ptr(x), ptr(ln_w), ptr(ln_b), ptr(wq_raw), ptr(bq), ptr(k), ptr(v), B,
-                                        Tq, T, H, precision, ptr(out)))
     return out
 
 
@@ -312,6 +297,13 @@ class WhisperModel:
         """True once a transcribe overflowed the LayerNorm fold's operand range
         and the model switched to the LayerNorm path (wa_model_wide_range)."""
         return lib().wa_model_wide_range(self._h) == 1
+
+    def set_fused_projections(self, on: bool) -> bool:
+        """Diagnostics (wa_model_set_fused_projections): few-clip decode steps
+        form the qkv / cross-attention query projections inside the attention
+        launches (default) or run the GEMM launches.  Returns the previous
+        setting."""
+        return lib().wa_model_set_fused_projections(self._h, 1 if on else 0) == 1
 
     def device_bytes(self) -> int:
         return int(lib().wa_model_device_bytes(self._h))
