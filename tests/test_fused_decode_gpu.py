@@ -1,7 +1,9 @@
-"""In-launch projections of the few-clip decode step (wa_headproj.hpp,
-VERDICT r03 item 2): the decoder self-attention forms its head's q / k / v and
-the K / V cross-attention its query inside their own launches, replacing the
-qkv and cq GEMM launches (decoder.rs:77-112, attention.rs:93-125,208-236).
+"""In-launch projections of the decode step (wa_headproj.hpp, VERDICT r03
+item 2): in few-clip groups the decoder self-attention forms its head's q / k
+/ v and the K / V cross-attention its query inside their own launches,
+replacing the qkv and cq GEMM launches; in groups of up to 16 clips on the
+encoder planes the cross-attention's query transform forms the query itself,
+replacing the cq GEMM launch (decoder.rs:77-112, attention.rs:93-125,208-236).
 
 The fused kernels reproduce the decode-step GEMM's arithmetic (wq4_skinny.hip)
 exactly, so under kernel policy 3 (every <= 32-row GEMM on that kernel) a
@@ -27,7 +29,7 @@ def _trace_ids(B: int, steps: int, V: int) -> np.ndarray:
     return rng.integers(0, V, size=(B, steps + 1, 16), dtype=np.int32)
 
 
-def _run(m, mel, ids, lang, steps, fused: bool):
+def _run(m, mel, ids, lang, steps, fused: int):
     prev = m.set_fused_projections(fused)
     try:
         return m.transcribe_trace(mel, ids, lang, steps, eot_stop=False)
@@ -40,6 +42,9 @@ def _run(m, mel, ids, lang, steps, fused: bool):
     ("tiny_test", 80, 3, None, 24),    # three clips, auto language
     ("medium", 80, 1, 50259, 16),      # D = 1024, H = 16
     ("large_v3", 128, 2, 50259, 16),   # D = 1280, H = 20: the product's one/two-clip decode
+    ("tiny_test", 80, 16, 50259, 24),  # a 16-clip group on the encoder planes: the fused query transform
+    ("tiny_test", 80, 11, None, 24),   # 11 rows of the 16-row tile, auto language
+    ("large_v3", 128, 16, 50259, 8),   # the bench's decode-group shape
 ])
 def test_fused_projections_bit_identical_under_policy3(variant, n_mels, B, lang, steps):
     import torch
@@ -53,13 +58,14 @@ def test_fused_projections_bit_identical_under_policy3(variant, n_mels, B, lang,
     ids = _trace_ids(B, steps, V)
     wq4.set_kernel_policy(3)
     try:
-        t_gemm, l_gemm = _run(m, mel, ids, lang, steps, fused=False)
-        t_fused, l_fused = _run(m, mel, ids, lang, steps, fused=True)
+        t_gemm, l_gemm = _run(m, mel, ids, lang, steps, fused=0)
+        runs = {mask: _run(m, mel, ids, lang, steps, fused=mask) for mask in (1, 2, 3)}
     finally:
         wq4.set_kernel_policy(0)
-    assert t_fused == t_gemm
-    assert np.array_equal(l_fused[:, 1:], l_gemm[:, 1:], equal_nan=True), \
-        float(np.nanmax(np.abs(l_fused[:, 1:] - l_gemm[:, 1:])))
+    for mask, (t_fused, l_fused) in runs.items():
+        assert t_fused == t_gemm, mask
+        assert np.array_equal(l_fused[:, 1:], l_gemm[:, 1:], equal_nan=True), \
+            (mask, float(np.nanmax(np.abs(l_fused[:, 1:] - l_gemm[:, 1:]))))
     m.close()
 
 

@@ -1,8 +1,7 @@
 """The product's environment tuning knobs, each run end to end (GPU).
 
-Every knob only re-plans work the default path already does -- a different
-decode-GEMM plan (wq4_q4gemm.hip plan_decode: WQ4_DECODE_W8, _PER8, _PER,
-_MAXKS), the LayerNorm fold off (wa_model.cpp lnfold_on: WA_LN_FOLD),
+Every knob only re-plans work the default path already does -- the
+LayerNorm fold off (wa_model.cpp lnfold_on: WA_LN_FOLD),
 another number of decode groups (wa_model.cpp decode_groups:
 WA_DECODE_GROUPS) or the cross-attention over cached K / V for more clips
 (wa_model.cpp kv_config: WA_XATTN_KV_CLIPS, whose groups then also form
@@ -28,10 +27,7 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 KNOBS = [
     {},
-    {"WQ4_DECODE_W8": "0"},                               # 4-wave decode plans
-    {"WQ4_DECODE_W8": "0", "WQ4_DECODE_PER": "1"},        # 4-wave, most K slices
-    {"WQ4_DECODE_W8": "0", "WQ4_DECODE_MAXKS": "1"},      # 4-wave, no split-K
-    {"WQ4_DECODE_PER8": "1"},                             # 8-wave with K slices
+    {"WQ4_KERNEL_POLICY": "3"},                           # every <= 32-row GEMM on the decode-step kernel
     {"WA_LN_FOLD": "0"},                                  # LayerNorm as its own pass
     {"WA_DECODE_GROUPS": "1"},
     {"WA_DECODE_GROUPS": "3"},                            # ragged groups 6/5/5
@@ -42,7 +38,7 @@ KNOBS = [
 
 def _run(env_over):
     env = dict(os.environ)
-    for k in ("WQ4_DECODE_W8", "WQ4_DECODE_PER8", "WQ4_DECODE_PER", "WQ4_DECODE_MAXKS", "WA_LN_FOLD",
+    for k in ("WQ4_KERNEL_POLICY", "WA_LN_FOLD",
               "WA_DECODE_GROUPS", "WA_XATTN_KV_CLIPS"):
         env.pop(k, None)
     env.update(env_over)

@@ -564,22 +564,26 @@ __global__ __launch_bounds__(512) void dec_self_attn_fused_kernel(HeadProj p, fl
   const int kv_len = state->kv_len;
   const size_t hb = ((size_t)b * H + head) * ctx * 64;
   auto sub_of = [&](int s) { return (s >> 2) * (D / 16) + 4 * head + (s & 3); };
-  (void)hp_issue<12>(p, sub_of, b, smem, wave, 8, lane);
+  hp_issue<1, 12>(p, sub_of, b, 1, smem, wave, 8, lane);
   vmcnt_wait<0>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if (wave == 0) {
     float mean, den;
-    hp_row_stats<12>(p, smem, lane, mean, den);
+    hp_row_stats<1, 12>(p, smem, 0, lane, mean, den);
     if (lane == 0) {
       srow[0] = mean;
       srow[1] = den;
     }
   }
-  hp_compute<12>(p, smem, wave, 8, lane);
+  {
+    floatx4 acc[1][12];
+    hp_compute<1, 12, 1>(p, smem, wave, 8, lane, acc);
+    hp_store_red<1, 12, 1>(p, smem, wave, 8, lane, acc);
+  }
   __syncthreads();
   if (tid < 192) {
-    const float y = hp_finish<12>(p, smem, tid, srow[0], srow[1]);
+    const float y = hp_finish<1, 12>(p, smem, 0, tid, srow[0], srow[1]);
     const int part = tid >> 6, d = tid & 63;
     qkv_s[part][d] = y;
     // append k, v (decoder.rs:77-112 via Tensor::cat); read back from LDS below
@@ -642,14 +646,14 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
   return hipGetLastError();
 }
 
-bool fused_proj_supported(int D, int ns) { return ns == 2 && hp_supported(12, D) && hp_supported(4, D); }
+bool fused_proj_supported(int D, int ns) { return ns == 2 && hp_supported(1, 12, D) && hp_supported(1, 4, D); }
 
 hipError_t launch_decoder_self_attention_fused(const HeadProj& p, float* cache_k, float* cache_v, int B, int H, int ctx,
                                                const DecodeState* state, _Float16* tiled, int ns, hipStream_t st) {
   if (!state || ctx > kMaxCtx || H * 64 != p.K || !fused_proj_supported(p.K, ns) || !p.q16 || !p.d16 || !p.at ||
       !p.stats || !p.wg || !p.b2 || p.ku * 128 != p.K)
     return hipErrorInvalidValue;
-  const size_t lds = hp_lds_bytes(12, p.ku);
+  const size_t lds = hp_lds_bytes(1, 12, p.ku);
   hipLaunchKernelGGL((dec_self_attn_fused_kernel<2>), dim3(H, B), dim3(512), lds, st, p, cache_k, cache_v, H, ctx,
                      state, tiled);
   return hipGetLastError();
@@ -727,7 +731,7 @@ __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restr
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ float qs[64];
     __shared__ float srow[2];
-    (void)hp_issue<4>(fq, [&](int s) { return 4 * head + s; }, b, smem, wave, 4, lane);
+    hp_issue<1, 4>(fq, [&](int s) { return 4 * head + s; }, b, 1, smem, wave, 4, lane);
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     floatx4 kk[U], vv[U];  // the first pass of K / V, in flight behind the LDS-DMA
@@ -737,15 +741,19 @@ __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restr
     asm volatile("" ::: "memory");
     if (wave == 0) {
       float mean, den;
-      hp_row_stats<4>(fq, smem, lane, mean, den);
+      hp_row_stats<1, 4>(fq, smem, 0, lane, mean, den);
       if (lane == 0) {
         srow[0] = mean;
         srow[1] = den;
       }
     }
-    hp_compute<4>(fq, smem, wave, 4, lane);
+    {
+      floatx4 acc[2][4];
+      hp_compute<1, 4, 2>(fq, smem, wave, 4, lane, acc);
+      hp_store_red<1, 4, 2>(fq, smem, wave, 4, lane, acc);
+    }
     __syncthreads();
-    if (tid < 64) qs[tid] = hp_finish<4>(fq, smem, tid, srow[0], srow[1]);
+    if (tid < 64) qs[tid] = hp_finish<1, 4>(fq, smem, 0, tid, srow[0], srow[1]);
     __syncthreads();
     qv[0] = *reinterpret_cast<const floatx4*>(&qs[sub * 4]) * kEaQScale;
     if (j0 < k1) attn_update<TQ, U>(qv, Tq, j0, k1, grp, [](int, int) { return true; }, kk, vv, m, l, o);
@@ -837,7 +845,7 @@ hipError_t launch_cross_attention_kv(const float* q, const float* k, const float
   hipLaunchKernelGGL((cross_attn_kv_kernel<NS_, TQ_, F_>), grid, block, LDS_, st, q, k, v, Tq, T, H, S, part, \
                      counters, tiled, fq)
   if (fuse) {
-    WA_XKV(2, 1, true, (size_t)hp_lds_bytes(4, fuse->ku));
+    WA_XKV(2, 1, true, (size_t)hp_lds_bytes(1, 4, fuse->ku));
   } else if (ns == 2) {
     if (Tq == 1) { WA_XKV(2, 1, false, 0); } else { WA_XKV(2, 4, false, 0); }
   } else {

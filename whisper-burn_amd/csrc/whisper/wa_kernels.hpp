@@ -82,10 +82,15 @@ size_t xattn_part_floats(int R, int H, int D, int T);
 // projection's lane order (same bytes; wv_pack_words u32 words).
 size_t wv_pack_words(int H, int D);
 hipError_t launch_wv_pack(const uint8_t* wv, int H, int D, uint32_t* out, hipStream_t st);
-// wvp: the launch_wv_pack words of wv (Q4 weights; ignored for f16 weights)
+// wvp: the launch_wv_pack words of wv (Q4 weights; ignored for f16 weights).
+// With fuse != nullptr (decode steps of <= 16 clips, Q4_0, f16x2:
+// xattn_fused_q_supported) q is not read: the query transform forms each
+// head's query from the cq weight (the cross_attn_ln fold) in the same
+// launch -- the same bits as the cq GEMM under kernel policy 3.
+bool xattn_fused_q_supported(int R, int Tq, int D, int wtype, int ns);
 hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, const uint32_t* wvp, const float* bv,
                         int wtype, const _Float16* enc, int B, int Tq, int T, int H, int D, _Float16* qt, float* part,
-                        _Float16* tiled, int ns, hipStream_t st);
+                        _Float16* tiled, int ns, hipStream_t st, const HeadProj* fuse = nullptr);
 // A-tiled operand [R][K] (hi + lo) -> f32 rows (diagnostics).
 hipError_t launch_untile(const _Float16* tiled, int R, int K, int ns, float* out, hipStream_t st);
 // f32 rows [rows][D] -> [rows][ns][D] f16 planes (hi | lo) for launch_xattn.

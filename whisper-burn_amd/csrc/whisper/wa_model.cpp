@@ -200,6 +200,9 @@ struct DecGroup {
 
 }  // namespace
 
+// the decode step's in-launch projections on by default (measured: DESIGN.md §4)
+constexpr int kFuseSelf = 1, kFuseCrossQ = 2, kFuseDefault = kFuseCrossQ;
+
 struct wa_model {
   int device = 0;
   Config cfg{};
@@ -229,10 +232,9 @@ struct wa_model {
   // Cross K / V caches (capacity kv_clips clips) for transcribes of at most
   // kv_small clips -- their decode steps are launch-latency chains: one GEMV
   // launch over the caches replaces the cache-free cross-attention's four,
-  // wa_kernels.hip -- or, for larger ones, the first kv_prefix clips (A/B
-  // knob).  kv_n: clips [0, kv_n) of the last encoder pass have caches; a
-  // decode group entirely inside them reads the caches.
-  int kv_clips = 0, kv_small = 0, kv_prefix = 0;
+  // wa_kernels.hip.  kv_n: clips [0, kv_n) of the last encoder pass have
+  // caches; a decode group entirely inside them reads the caches.
+  int kv_clips = 0, kv_small = 0;
   int kv_n = 0;
   bool group_kv(const DecGroup& g) const { return g.nb > 0 && g.b0 + g.nb <= kv_n; }
   hipStream_t own_stream = nullptr;  // encoder / encoder planes (graph capture needs a non-null stream)
@@ -246,10 +248,12 @@ struct wa_model {
   // |beta|); still flagged -> WQ4_ERANGE, never NaN tokens.
   int* range_flag = nullptr;
   bool wide_range = false;
-  // few-clip decode steps form the qkv / cq projections inside the attention
-  // launches (wa_headproj.hpp); off only for the bit-equality test
-  // (wa_model_set_fused_projections)
-  bool fuse_proj = true;
+  // decode steps form projections inside the attention launches
+  // (wa_headproj.hpp): bit 0 the few-clip self-attention's q / k / v, bit 1
+  // the cross-attention query (few-clip K / V form and <= 16-clip groups on
+  // the encoder planes); wa_model_set_fused_projections (diagnostics, the
+  // bit-equality test)
+  int fuse_proj = kFuseDefault;
   float timings[5] = {0, 0, 0, 0, 0};
   // decode-step logit trace (wa_transcribe_trace; null otherwise): device
   // [clip][trace_s1][trace_k] ids and their logits
@@ -837,7 +841,7 @@ wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st) {
   const int64_t rows = (int64_t)B * c.n_audio_ctx;
   m->kv_batch = B;
   WA_HIP(wa::launch_enc_planes(m->enc_f32, rows, c.n_audio_state, m->ns, m->enc_planes, st));
-  m->kv_n = std::min(B <= m->kv_small ? B : m->kv_prefix, m->kv_clips);
+  m->kv_n = B <= m->kv_small ? B : 0;
   if (m->kv_n > 0) {
     // ln_post again, as the GEMMs' A-tiled operand (m->x still holds its
     // input); the caches of clips [0, kv_n): a prefix of the rows
@@ -902,9 +906,15 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
     // q / k / v and the K / V cross-attention its query inside their own
     // launches from the LayerNorm-fold operand (wa_headproj.hpp) -- the qkv
     // and cq GEMM launches leave the chain, the values are the same bits
-    const bool fuse = fold && m->fuse_proj && m->group_kv(g) && L.qkv_q16 != nullptr && L.cq_q16 != nullptr &&
-                      wa::fused_proj_supported(D, m->ns);
-    if (fuse) {
+    const bool proj = fold && L.qkv_q16 != nullptr && L.cq_q16 != nullptr;
+    const bool kvf = proj && m->group_kv(g) && wa::fused_proj_supported(D, m->ns);
+    const bool fuse_sa = kvf && (m->fuse_proj & kFuseSelf);
+    const bool fuse = kvf && (m->fuse_proj & kFuseCrossQ);  // the K / V cross-attention's query
+    // groups of <= 16 clips streaming the encoder planes: the cross-attention
+    // query transform forms the query itself (xattn_q_fused_kernel)
+    const bool fuse_xq = proj && (m->fuse_proj & kFuseCrossQ) && !m->group_kv(g) &&
+                         wa::xattn_fused_q_supported((int)rows, Tq, D, m->wtype, m->ns);
+    if (fuse_sa) {
       const wa::HeadProj hp{L.qkv_q16, L.qkv_d16, (int)L.proj_ku, g.atd_ln, g.ln_stats, L.qkv_wg, L.qkv_b2, D};
       WA_HIP(wa::launch_decoder_self_attention_fused(hp, L.cache_k + self_ofs, L.cache_v + self_ofs, B, H,
                                                      c.n_text_ctx, state, g.atd_dec, m->ns, st));
@@ -924,7 +934,7 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
       const wq4_ln_fold prod2{L.ln2_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
       WA_WQ4(wq4_gemm_tiled_lnfold(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec,
                                    &prod2, st));
-      if (!fuse) {
+      if (!fuse && !fuse_xq) {
         const wq4_ln_fold cons2{nullptr, nullptr, nullptr, g.ln_stats, L.cq_wg};
         WA_WQ4(wq4_gemm_tiled_lnfold(L.cq, L.cq_b2, g.atd_ln, nullptr, g.qd, nullptr, rows, 0u, m->prec, &cons2, st));
       }
@@ -933,14 +943,14 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
       WA_WQ4(wq4_layernorm(g.xd, L.ln2_w, L.ln2_b, rows, D, m->prec, g.atd_dec, nullptr, st));
       WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, g.atd_dec, nullptr, g.qd, nullptr, rows, 0u, m->prec, 2, st));
     }
+    const wa::HeadProj hq{L.cq_q16, L.cq_d16, (int)L.proj_ku, g.atd_ln, g.ln_stats, L.cq_wg, L.cq_b2, D};
     if (m->group_kv(g)) {  // few clips: one GEMV launch over the cached K / V
       const size_t kofs = (size_t)g.b0 * T * D;
-      const wa::HeadProj hq{L.cq_q16, L.cq_d16, (int)L.proj_ku, g.atd_ln, g.ln_stats, L.cq_wg, L.cq_b2, D};
       WA_HIP(wa::launch_cross_attention_kv(fuse ? nullptr : g.qd, L.xk + kofs, L.xv + kofs, B, Tq, T, H, g.xkv_part,
                                            g.xkv_ctr, g.atd_dec, m->ns, st, fuse ? &hq : nullptr));
     } else {
-      WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, Tq, T, H, D, g.xqt,
-                              g.xattn_part, g.atd_dec, m->ns, st));
+      WA_HIP(wa::launch_xattn(fuse_xq ? nullptr : g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, Tq, T, H,
+                              D, g.xqt, g.xattn_part, g.atd_dec, m->ns, st, fuse_xq ? &hq : nullptr));
     }
     if (fold) {
       const wq4_ln_fold prod3{L.ln3_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
@@ -1054,7 +1064,7 @@ wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
   // encoder-plane offsets), the EOT mode and the trace buffers
   const int64_t key =
       (((((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0)) * 2 +
-       (m->group_kv(g) ? 1 : 0)) * 4 + (m->wide_range ? 1 : 0) + (m->fuse_proj ? 2 : 0);
+       (m->group_kv(g) ? 1 : 0)) * 8 + (m->wide_range ? 1 : 0) + 2 * m->fuse_proj;
   if (g.graph && g.graph_key == key) return WQ4_OK;
   if (g.graph) {
     (void)hipGraphExecDestroy(g.graph);
@@ -1075,21 +1085,14 @@ wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
 }
 
 // Clips up to which a transcribe decodes over cross K / V caches
-// (WA_XATTN_KV_CLIPS overrides; 0 = never; measured in DESIGN.md §4), and
-// WA_XATTN_KV_PREFIX: larger transcribes give their first that many clips
-// caches too (A/B knob; 0 by default).
+// (WA_XATTN_KV_CLIPS overrides; 0 = never; measured in DESIGN.md §4).
 void kv_config(wa_model* m, int max_batch) {
   static const int small = [] {
     const char* e = getenv("WA_XATTN_KV_CLIPS");
     return e ? std::max(0, atoi(e)) : 8;
   }();
-  static const int prefix = [] {
-    const char* e = getenv("WA_XATTN_KV_PREFIX");
-    return e ? std::max(0, atoi(e)) : 0;
-  }();
   m->kv_small = std::min(small, max_batch);
-  m->kv_prefix = std::min(prefix, max_batch);
-  m->kv_clips = std::max(m->kv_small, m->kv_prefix);
+  m->kv_clips = m->kv_small;
 }
 
 // Number of decode groups for a batch (WA_DECODE_GROUPS overrides).
@@ -1478,10 +1481,10 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
 
 int wa_model_wide_range(const wa_model* m) { return m ? (m->wide_range ? 1 : 0) : -1; }
 
-int wa_model_set_fused_projections(wa_model* m, int on) {
-  if (!m) return -1;
-  const int prev = m->fuse_proj ? 1 : 0;
-  m->fuse_proj = on != 0;
+int wa_model_set_fused_projections(wa_model* m, int mask) {
+  if (!m || mask < -1 || mask > 3) return -1;
+  const int prev = m->fuse_proj;
+  m->fuse_proj = mask < 0 ? kFuseDefault : mask;
   return prev;
 }
 

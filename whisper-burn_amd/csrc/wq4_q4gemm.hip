@@ -857,7 +857,7 @@ __global__ __launch_bounds__(64 * W) void q4_gemm_decode_kernel(const uint8_t* _
         const int rl = acc_row(i, h);
         const int row = (mt0 + mt) * 32 + rl;
         float a = v[q] * cs;
-        if (e.lnf_stats_in) a = (a - lnf_mu[rl] * pre_wg) / lnf_den[rl];  // LayerNorm fold, consumer
+        if (e.lnf_stats_in) a = lnf_apply(a, lnf_mu[rl], pre_wg, lnf_den[rl]);  // LayerNorm fold, consumer
         if constexpr (EPI == kEpiTiled) {
           stage[rl * kStageLd + r] = (row < e.m && col < e.n) ? epi_value_pre(a, pre_bias, pre_res[q], e) : 0.0f;
         } else if constexpr (EPI == kEpiHeadMajor) {
@@ -1009,19 +1009,11 @@ DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal) {
   DecodePlan p{1, 1, 1, kDecodeWaves};
   (void)mreal;  // the plan depends on (N, K) only: batch-invariant rows
   // K <= 1536: one 8-wave workgroup per n-tile holds the whole K range (no
-  // split-K hand-off at all); the grid is N / 32 workgroups.
-  static const bool w8 = [] {
-    const char* env = getenv("WQ4_DECODE_W8");  // tuning knob (tools/q4_bench.py)
-    return env ? atoi(env) != 0 : true;
-  }();
-  // block pairs per wave of the 8-wave plan before K is split over
-  // workgroups (tuning knob WQ4_DECODE_PER8: fewer = more, smaller slices)
-  static const int per8 = [] {
-    const char* env = getenv("WQ4_DECODE_PER8");
-    const int v = env ? atoi(env) : kDecodeMaxPer8;
-    return v >= 1 && v <= kDecodeMaxPer8 ? v : kDecodeMaxPer8;
-  }();
-  if (w8 && nbp <= 8 * per8 * kDecodeMaxKs && ntiles <= kDecodeMaxTiles) {
+  // split-K hand-off at all); the grid is N / 32 workgroups.  Measured and
+  // not kept (DESIGN.md dead ends): 4-wave plans and more, smaller K slices
+  // (fewer block pairs per wave) for every Whisper decode shape.
+  constexpr int per8 = kDecodeMaxPer8;
+  if (nbp <= 8 * per8 * kDecodeMaxKs && ntiles <= kDecodeMaxTiles) {
     // larger K: the same 8-wave workgroups over ks K slices (sc1 slabs +
     // last-arriver merge); ks depends on K only
     p.w = 8;
@@ -1042,19 +1034,7 @@ DecodePlan plan_decode(int64_t ntiles, int64_t nbp, int mreal) {
       break;
     }
   }
-  static const int forced = [] {  // tuning knob (tools/q4_bench.py)
-    const char* env = getenv("WQ4_DECODE_PER");
-    const int v = env ? atoi(env) : 0;
-    return (v == 1 || v == 2 || v == 4) ? v : 0;
-  }();
-  if (forced) per = forced > max_per ? max_per : forced;
-  static const int64_t max_ks = [] {  // tuning knob: cap the K slices (1 = no split)
-    const char* env = getenv("WQ4_DECODE_MAXKS");
-    const int v = env ? atoi(env) : 0;
-    return (int64_t)(v > 0 ? v : 1 << 20);
-  }();
   int64_t ks = (nbp + (int64_t)kDecodeWaves * per - 1) / ((int64_t)kDecodeWaves * per);
-  if (ks > max_ks) ks = max_ks;
   if (ks > kDecodeMaxKs) ks = kDecodeMaxKs;
   while (ks > 1 && ntiles * ks * 2 * 1024 > (int64_t)kDecodeWsFloats) --ks;  // workspace bound (2 m-tiles)
   if (ntiles > kDecodeMaxTiles) ks = 1;

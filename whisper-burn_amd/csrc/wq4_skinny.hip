@@ -365,7 +365,7 @@ __global__ __launch_bounds__(64 * kSkW) void skinny_gemm_kernel(const uint32_t* 
     const int o = tid + 512 * j, lr = o / COLS, orow = r0 + lr, ocol = o % COLS, n = nt * COLS + ocol;
     const bool ok = o < OUT && orow < e.m && n < e.n;
     float a = sum[j] * ainv;
-    if (e.lnf_stats_in && o < OUT) a = (a - lnf_mu[lr] * pre_wg[j]) / lnf_den[lr];  // LayerNorm fold, consumer
+    if (e.lnf_stats_in && o < OUT) a = lnf_apply(a, lnf_mu[lr], pre_wg[j], lnf_den[lr]);  // LayerNorm fold, consumer
     y[j] = ok ? epi_value_pre(a, pre_bias[j], pre_res[j], e) : 0.0f;
     if constexpr (EPI == kEpiF32) {
       if (ok) e.out[(size_t)orow * e.ldo + n] = y[j];

@@ -298,12 +298,15 @@ class WhisperModel:
         and the model switched to the LayerNorm path (wa_model_wide_range)."""
         return lib().wa_model_wide_range(self._h) == 1
 
-    def set_fused_projections(self, on: bool) -> bool:
-        """Diagnostics (wa_model_set_fused_projections): few-clip decode steps
-        form the qkv / cross-attention query projections inside the attention
-        launches (default) or run the GEMM launches.  Returns the previous
-        setting."""
-        return lib().wa_model_set_fused_projections(self._h, 1 if on else 0) == 1
+    def set_fused_projections(self, mask: int) -> int:
+        """Diagnostics (wa_model_set_fused_projections): bit 0 the few-clip
+        self-attention's q / k / v, bit 1 the cross-attention query formed
+        inside the attention launches; -1 = the product default.  Returns the
+        previous mask."""
+        prev = lib().wa_model_set_fused_projections(self._h, int(mask))
+        if prev < 0:
+            raise ValueError(f"bad fused-projection mask {mask}")
+        return prev
 
     def device_bytes(self) -> int:
         return int(lib().wa_model_device_bytes(self._h))
