@@ -668,12 +668,7 @@ wq4_status alloc_activations(wa_model* m) {
   for (auto& L : m->dec) {
     L.cache_k = f32((int64_t)B * c.n_text_ctx * Dt);
     L.cache_v = f32((int64_t)B * c.n_text_ctx * Dt);
-    if (m->kv_clips > 0) {
-      L.xk = f32((int64_t)m->kv_clips * T * Dt);
-      L.xv = f32((int64_t)m->kv_clips * T * Dt);
-      if (!L.xk || !L.xv) return fail(WQ4_ENOMEM, "cross K/V cache allocation failed");
-    }
-  }
+  }  // the cross K / V caches: on the first transcribe that reads them (cross_kv_forward)
   // f16-pair tied embedding for the decode step's fused logits + pick,
   // fragment-tiled (1 KiB contiguous per load instruction)
   if (!wa::emb_tiled_supported(Dt)) return fail(WQ4_EINVAL, "n_text_state must be a multiple of 128");
@@ -836,12 +831,28 @@ wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st,
 // Transcribes of at most kv_clips clips also get the reference's own
 // per-layer caches, K = enc Wk^T and V = enc Wv^T + bv, head-major (the
 // few-clip decode reads them: launch_cross_attention_kv).
-wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st) {
+// `caches` false (wa_encode: no decode follows it) fills the planes only.
+// The caches (f32, kv_clips x n_audio_ctx x n_text_state per layer and
+// tensor: 3.9 GB for Large-V3 at 8 clips) are allocated on the first
+// transcribe of at most kv_small clips, so batches past that never hold them.
+wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st, bool caches) {
   const Config& c = m->cfg;
   const int64_t rows = (int64_t)B * c.n_audio_ctx;
   m->kv_batch = B;
   WA_HIP(wa::launch_enc_planes(m->enc_f32, rows, c.n_audio_state, m->ns, m->enc_planes, st));
-  m->kv_n = B <= m->kv_small ? B : 0;
+  m->kv_n = caches && B <= m->kv_small ? B : 0;
+  if (m->kv_n > 0 && m->dec[0].xk == nullptr) {
+    const size_t n = (size_t)m->kv_clips * c.n_audio_ctx * c.n_text_state;
+    for (DecLayer& L : m->dec) {
+      L.xk = m->dev.alloc<float>(n);
+      L.xv = m->dev.alloc<float>(n);
+      if (!L.xk || !L.xv) {
+        m->kv_n = 0;
+        return fail(WQ4_ENOMEM, "cross K/V cache allocation failed");
+      }
+      m->bytes += n * 8;
+    }
+  }
   if (m->kv_n > 0) {
     // ln_post again, as the GEMMs' A-tiled operand (m->x still holds its
     // input); the caches of clips [0, kv_n): a prefix of the rows
@@ -1283,7 +1294,7 @@ wq4_status wa_encode(wa_model* m, const float* mel_dev, int n_clips, float* enc_
   hipStream_t st = static_cast<hipStream_t>(stream);
   wq4_status s = encoder_forward(m, mel_dev, n_clips, st, enc_out_dev);
   if (s != WQ4_OK) return s;
-  return cross_kv_forward(m, n_clips, st);
+  return cross_kv_forward(m, n_clips, st, false);
 }
 
 wq4_status wa_prompt_logits(wa_model* m, const int32_t* prompt_dev, int n_clips, int plen, float* logits_dev,
@@ -1329,7 +1340,7 @@ wq4_status transcribe_once(wa_model* m, const float* mel_dev, int n_clips, int l
   wq4_status s = encoder_forward(m, mel_dev, B, st, nullptr);
   if (s != WQ4_OK) return s;
   WA_HIP(hipEventRecord(ev[1], st));
-  s = cross_kv_forward(m, B, st);
+  s = cross_kv_forward(m, B, st, true);
   if (s != WQ4_OK) return s;
   WA_HIP(hipEventRecord(ev[2], st));
 
@@ -1515,8 +1526,11 @@ int wa_decode_group_rows(int n_clips) {
   return (n_clips + G - 1) / G;  // the largest group (groups split [0, B) evenly, transcribe_batch)
 }
 
-wq4_status wa_probe_kernels(wa_model* m, int n_clips, int iters, double* out) {
+constexpr int kProbeOut = WA_PROBE_OUT;
+
+wq4_status wa_probe_kernels(wa_model* m, int n_clips, int iters, double* out, int out_len) {
   if (!m || !out) return fail(WQ4_EINVAL, "null argument");
+  if (out_len < kProbeOut) return fail(WQ4_EINVAL, "out holds fewer than 6 doubles");
   if (n_clips < 1 || n_clips > m->bmax || iters < 1) return fail(WQ4_EINVAL, "bad n_clips / iters");
   if (n_clips > m->kv_batch) return fail(WQ4_EINVAL, "run wa_transcribe / wa_encode on n_clips clips first");
   WA_HIP(hipSetDevice(m->device));
@@ -1524,7 +1538,7 @@ wq4_status wa_probe_kernels(wa_model* m, int n_clips, int iters, double* out) {
   const Config& c = m->cfg;
   const int B = n_clips, D = c.n_text_state, T = c.n_audio_ctx, H = c.n_text_head;
   DecLayer& L = m->dec[0];
-  DecGroup& g = m->groups[0];
+  DecGroup g = m->groups[0];  // group 0's buffers, a clip range of its own
   const _Float16* enc = m->enc_planes;
   hipEvent_t a, b;
   WA_HIP(hipEventCreate(&a));

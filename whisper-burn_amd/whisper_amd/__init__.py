@@ -46,7 +46,7 @@ def lib() -> ctypes.CDLL:
         L.wa_synth_uniform.argtypes = [ctypes.c_uint64, ctypes.c_char_p, c_i64, ctypes.c_float, ctypes.c_float, f32p]
         L.wa_profile_enable.argtypes = [vp, c_int]
         L.wa_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), c_int]
-        L.wa_probe_kernels.argtypes = [vp, c_int, c_int, ctypes.POINTER(ctypes.c_double)]
+        L.wa_probe_kernels.argtypes = [vp, c_int, c_int, ctypes.POINTER(ctypes.c_double), c_int]
         L.wa_decode_group_rows.argtypes = [c_int]
         L.wa_decode_group_rows.restype = c_int
         L.wa_model_create_synthetic_ex.argtypes = [c_int, c_int, ctypes.c_uint64, c_int, c_int, c_int,
@@ -377,7 +377,7 @@ class WhisperModel:
     def probe_kernels(self, n_clips: int, iters: int = 20) -> dict:
         """HIP-event timing of single decode-step kernels (after transcribe)."""
         buf = (ctypes.c_double * 6)()
-        check(lib().wa_probe_kernels(self._h, n_clips, iters, buf))
+        check(lib().wa_probe_kernels(self._h, n_clips, iters, buf, len(buf)))
         return {"cross_attention": {"us": buf[0], "bytes": buf[1], "kv_cache": buf[5] != 0.0},
                 "decode_fc1": {"us": buf[2], "bytes": buf[3], "flops": buf[4]}}
 
