@@ -46,12 +46,13 @@ task_suite() {
 
 task_bench() { bench_line bench $BENCH_ARGS; }
 
-task_configs() {
-  bench_line c2_medium_b1 --variant medium --clips-per-gpu 1 --no-cpu-baseline || return 1
-  bench_line c3_large_v3_b1 --clips-per-gpu 1 --no-cpu-baseline || return 1
-  bench_line c5_large_v3_f16w --weights f16 || return 1
-  bench_line c5_large_v3_f16w_b1 --weights f16 --clips-per-gpu 1 --no-cpu-baseline || return 1
-  bench_line c4_precision_f16 --precision f16 --no-cpu-baseline
+task_configs() {  # every line timed over 3 steps after 1 warmup
+  local S="--steps 3 --warmup 1"
+  bench_line c2_medium_b1 --variant medium --clips-per-gpu 1 --no-cpu-baseline $S || return 1
+  bench_line c3_large_v3_b1 --clips-per-gpu 1 --no-cpu-baseline $S || return 1
+  bench_line c5_large_v3_f16w --weights f16 --no-cpu-baseline $S || return 1
+  bench_line c5_large_v3_f16w_b1 --weights f16 --clips-per-gpu 1 --no-cpu-baseline $S || return 1
+  bench_line c4_precision_f16 --precision f16 --no-cpu-baseline $S
 }
 
 task_trace() {

@@ -1,0 +1,206 @@
+// Cost of one Q4_0 block (32 k) of a 32 x 32 output tile per wave, in the
+// encoder GEMM's exact f16x2 form against an int8-limb form (VERDICT r03
+// item 4), operands register-resident except the packed weight nibbles and
+// scales, which come from LDS as in the product kernels:
+//   f16x2   product form (wq4_enc.hip): dequantise 16 nibbles per lane to
+//           f16 (q - 8), four v_mfma_f32_32x32x16_f16 (hi and lo activation
+//           planes x two k halves) into a block temporary, then
+//           acc = fma(tmp, d, acc) per accumulator element
+//   limb    activations as three signed 8-bit limbs of a per-row 24-bit
+//           fixed-point mantissa: three v_mfma_i32_32x32x32_i8 (one per limb,
+//           k = 32 = the whole block), then per accumulator element
+//           (t0 << 14) + (t1 << 7) + t2 (two v_lshl_add), cvt to f32 and the
+//           block-scale fma -- the per-block scale is per (column, block), so
+//           the int32 sums cannot run across blocks
+//   *-mfma  the same MFMAs with no VALU work (the MFMA floor of each form)
+// Timed with many workgroups (every CU, 1 or 2 waves per SIMD); reported as
+// cycles per block per wave and as the dense-equivalent rate
+// 2 * 32 * 32 * 32 FLOP per block per wave.  Results are summed into a sink
+// so nothing is dead code.
+//
+//   hipcc --offload-arch=gfx950 -O3 -o tools/limb_micro tools/limb_micro.hip
+//   ./tools/limb_micro [blocks]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x)                                                                       \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef int intx16 __attribute__((ext_vector_type(16)));
+typedef int intx4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+enum Form { kF16x2 = 0, kLimb = 1, kF16Mfma = 2, kLimbMfma = 3 };
+
+template <class T>
+__device__ __forceinline__ void launder(T& x) {
+  asm volatile("" : "+v"(x));
+}
+
+// 16 nibbles (two u32) -> 16 f16 (q - 8) via the 0x6400 exponent trick
+__device__ __forceinline__ void deq_f16(u32x2 w, half8& lo, half8& hi) {
+  unsigned r[8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // nibbles 2j, 2j+1 of word i into two f16 lanes of 1024 + q
+      const unsigned x = (w[i] >> (8 * j)) & 0xffu;
+      r[4 * i + j] = ((x & 0xfu) | ((x & 0xf0u) << 12)) | 0x64006400u;
+    }
+  }
+  typedef _Float16 half2 __attribute__((ext_vector_type(2)));
+  const half2 off = half2{(_Float16)1032.0f, (_Float16)1032.0f};
+  half2 h[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h[i] = __builtin_bit_cast(half2, r[i]) - off;
+  lo = half8{h[0][0], h[0][1], h[1][0], h[1][1], h[2][0], h[2][1], h[3][0], h[3][1]};
+  hi = half8{h[4][0], h[4][1], h[5][0], h[5][1], h[6][0], h[6][1], h[7][0], h[7][1]};
+}
+
+// 16 nibbles -> 16 signed bytes (q - 8): (q ^ 8) - 8 per byte without carries
+// across bytes: ((v ^ 0x08..) | 0x80..) - 0x88.. then flip the top bit back
+__device__ __forceinline__ intx4 deq_i8(u32x2 w) {
+  intx4 r;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const unsigned lo = w[i] & 0x0f0f0f0fu, hi = (w[i] >> 4) & 0x0f0f0f0fu;
+    r[2 * i] = (int)(((lo | 0x80808080u) - 0x08080808u) ^ 0x80808080u);
+    r[2 * i + 1] = (int)(((hi | 0x80808080u) - 0x08080808u) ^ 0x80808080u);
+  }
+  return r;
+}
+
+template <int F>
+__global__ __launch_bounds__(256) void block_loop(int nblk, float* sink) {
+  __shared__ unsigned wq[1024];
+  __shared__ _Float16 ds[512];
+  const int tid = threadIdx.x, l = tid & 63;
+  for (int i = tid; i < 1024; i += 256) wq[i] = 0x9e3779b9u * (unsigned)(i + 1) + blockIdx.x;
+  for (int i = tid; i < 512; i += 256) ds[i] = (_Float16)(0.001f * (float)(i % 97 + 1));
+  __syncthreads();
+  floatx16 acc = {};
+  float sum = 0.0f;
+  if constexpr (F == kF16x2 || F == kF16Mfma) {
+    half8 a[4];  // hi / lo planes x two k halves
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[i][j] = (_Float16)(0.01f * (float)((l + i * 8 + j) % 17));
+    half8 b0 = a[0], b1 = a[1];
+    for (int k = 0; k < nblk; ++k) {
+      const u32x2 w = *reinterpret_cast<const u32x2*>(&wq[(2 * (k * 64 + l)) & 1023]);
+      const float d = (float)ds[(k * 7 + (l & 31)) & 511];
+      if constexpr (F == kF16x2) deq_f16(w, b0, b1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) launder(a[i]);
+      if constexpr (F == kF16Mfma) {
+        launder(b0);
+        launder(b1);
+      }
+      floatx16 t = {};
+      if constexpr (F == kF16Mfma) t = acc;  // the floor: one accumulation chain, no VALU
+      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b0, t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b1, t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2], b0, t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[3], b1, t, 0, 0, 0);
+      if constexpr (F == kF16x2) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = fmaf(t[e], d, acc[e]);
+      } else {
+        acc = t;
+      }
+    }
+  } else {
+    intx4 a[3];  // three limbs
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[i][j] = 0x01020304 * (l + i + j + 1);
+    intx4 b = a[0];
+    intx16 iacc = {};
+    for (int k = 0; k < nblk; ++k) {
+      const u32x2 w = *reinterpret_cast<const u32x2*>(&wq[(2 * (k * 64 + l)) & 1023]);
+      const float d = (float)ds[(k * 7 + (l & 31)) & 511];
+      if constexpr (F == kLimb) b = deq_i8(w);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) launder(a[i]);
+      if constexpr (F == kLimbMfma) launder(b);
+      if constexpr (F == kLimbMfma) {  // the floor: one accumulation chain, no VALU
+        iacc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[0], b, iacc, 0, 0, 0);
+        iacc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[1], b, iacc, 0, 0, 0);
+        iacc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[2], b, iacc, 0, 0, 0);
+      } else {
+        const intx16 z = {};
+        const intx16 t0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[0], b, z, 0, 0, 0);
+        const intx16 t1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[1], b, z, 0, 0, 0);
+        const intx16 t2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[2], b, z, 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int c = (t0[e] << 14) + (t1[e] << 7) + t2[e];
+          acc[e] = fmaf((float)c, d, acc[e]);
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sum += (float)iacc[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) sum += acc[e];
+  if (sum == 1234.5f) sink[blockIdx.x] = sum;  // never true; keeps the loop alive
+}
+
+template <int F>
+double run(int wgs, int waves, int nblk, float* sink) {
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  hipLaunchKernelGGL(block_loop<F>, dim3(wgs), dim3(64 * waves), 0, nullptr, 16, sink);
+  CHECK(hipEventRecord(a, nullptr));
+  hipLaunchKernelGGL(block_loop<F>, dim3(wgs), dim3(64 * waves), 0, nullptr, nblk, sink);
+  CHECK(hipEventRecord(b, nullptr));
+  CHECK(hipEventSynchronize(b));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
+  return ms;
+}
+
+int main(int argc, char** argv) {
+  const int nblk = argc > 1 ? atoi(argv[1]) : 20000;
+  if (nblk < 1 || nblk > 1000000) return 2;
+  hipDeviceProp_t prop;
+  CHECK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+  float* sink = nullptr;
+  CHECK(hipMalloc(&sink, sizeof(float) * 8 * cus));
+  const char* names[4] = {"f16x2", "limb", "f16x2-mfma", "limb-mfma"};
+  const double clk = prop.clockRate * 1e3;  // Hz
+  for (int per_simd = 1; per_simd <= 2; ++per_simd) {
+    const int waves = 4 * per_simd, wgs = cus;
+    for (int f = 0; f < 4; ++f) {
+      const double ms = f == 0   ? run<kF16x2>(wgs, waves, nblk, sink)
+                        : f == 1 ? run<kLimb>(wgs, waves, nblk, sink)
+                        : f == 2 ? run<kF16Mfma>(wgs, waves, nblk, sink)
+                                 : run<kLimbMfma>(wgs, waves, nblk, sink);
+      const double blocks = (double)wgs * waves * nblk;
+      const double cyc = ms * 1e-3 * clk / ((double)nblk * per_simd);  // SIMD cycles per block (at clockRate)
+      const double tf = blocks * 2.0 * 32 * 32 * 32 / (ms * 1e-3) / 1e12;
+      printf("%-11s waves/SIMD %d  %8.3f ms  %6.1f SIMD-cycles per block  %7.1f TF/s-equiv\n", names[f], per_simd,
+             ms, cyc, tf);
+    }
+  }
+  CHECK(hipFree(sink));
+  return 0;
+}
