@@ -59,7 +59,7 @@ def test_fused_projections_bit_identical_under_policy3(variant, n_mels, B, lang,
     wq4.set_kernel_policy(3)
     try:
         t_gemm, l_gemm = _run(m, mel, ids, lang, steps, fused=0)
-        runs = {mask: _run(m, mel, ids, lang, steps, fused=mask) for mask in (1, 2, 3)}
+        runs = {mask: _run(m, mel, ids, lang, steps, fused=mask) for mask in (1, 2, 3, 5, 7)}
     finally:
         wq4.set_kernel_policy(0)
     for mask, (t_fused, l_fused) in runs.items():

@@ -49,6 +49,14 @@ bool fused_proj_supported(int D, int ns);
 // the qkv GEMM launch and this attention in one launch, the same bits.
 hipError_t launch_decoder_self_attention_fused(const HeadProj& p, float* cache_k, float* cache_v, int B, int H, int ctx,
                                                const DecodeState* state, _Float16* tiled, int ns, hipStream_t st);
+// The same, the projection spread over 8 workgroups per (head, clip) (the
+// decode-step GEMM's K split) whose last arriver finishes it and runs the
+// attention; part: self_attention_split_part_floats floats, ctr: B * H ints
+// zeroed once (re-armed by the kernel).  The same bits.
+size_t self_attention_split_part_floats(int B, int H);
+hipError_t launch_decoder_self_attention_split(const HeadProj& p, float* part, int* ctr, float* cache_k,
+                                               float* cache_v, int B, int H, int ctx, const DecodeState* state,
+                                               _Float16* tiled, int ns, hipStream_t st);
 
 // Cross-attention over cached K / V (attention.rs:177-236, the reference's
 // form; used for decode groups of a few clips): q [B*Tq, D] f32, k / v

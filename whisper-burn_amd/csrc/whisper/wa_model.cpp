@@ -187,6 +187,8 @@ struct DecGroup {
   float* xattn_part;  // cross-attention split partials (Z, max, sum)
   float* xkv_part;    // cross-attention over cached K / V: split partials
   int* xkv_ctr;       //   and the per-(clip, head) arrival counters
+  float* sa_part;     // split self-attention (dec_self_attn_split_kernel): partials
+  int* sa_ctr;        //   and the per-(clip, head) arrival counters
   _Float16* atd_ln;   // LayerNorm fold: A-tiled x * gamma of the next LayerNorm
   float* ln_stats;    //                 its per (row, 32-column tile) mean / M2
   _Float16* hid_t;    // fused logits + argmax: the final LN, A-tiled (m-tile 0)
@@ -201,7 +203,7 @@ struct DecGroup {
 }  // namespace
 
 // the decode step's in-launch projections on by default (measured: DESIGN.md §4)
-constexpr int kFuseSelf = 1, kFuseCrossQ = 2, kFuseDefault = kFuseCrossQ;
+constexpr int kFuseSelf = 1, kFuseCrossQ = 2, kFuseSelfSplit = 4, kFuseDefault = kFuseCrossQ;
 
 struct wa_model {
   int device = 0;
@@ -249,7 +251,8 @@ struct wa_model {
   int* range_flag = nullptr;
   bool wide_range = false;
   // decode steps form projections inside the attention launches
-  // (wa_headproj.hpp): bit 0 the few-clip self-attention's q / k / v, bit 1
+  // (wa_headproj.hpp): bit 0 the few-clip self-attention's q / k / v (bit 2:
+  // spread over 8 workgroups per head, dec_self_attn_split_kernel), bit 1
   // the cross-attention query (few-clip K / V form and <= 16-clip groups on
   // the encoder planes); wa_model_set_fused_projections (diagnostics, the
   // bit-equality test)
@@ -700,6 +703,8 @@ wq4_status alloc_activations(wa_model* m) {
     const int kvc = std::max(1, m->kv_clips);
     g.xkv_part = f32((int64_t)wa::cross_attention_kv_part_floats(kvc, c.n_text_head, T));
     g.xkv_ctr = d.alloc<int>((size_t)kvc * c.n_text_head);
+    g.sa_part = f32((int64_t)wa::self_attention_split_part_floats(kvc, c.n_text_head));
+    g.sa_ctr = d.alloc<int>((size_t)kvc * c.n_text_head);
     g.xqt = d.alloc<_Float16>((size_t)rdec * m->ns * HP * Dt);
     g.atd_ln = tiled(rdec, Dt);
     g.ln_stats = f32(rdec * (Dt / 16) * 2);  // per 16-column tile (the decode-step GEMM)
@@ -712,9 +717,10 @@ wq4_status alloc_activations(wa_model* m) {
                     (void*)g.atf_dec, (void*)g.prompt_tok, (void*)g.next_tok, (void*)g.tokens, (void*)g.ntok,
                     (void*)g.done, (void*)g.state, (void*)g.xattn_part, (void*)g.xqt, (void*)g.lg_val,
                     (void*)g.lg_idx, (void*)g.lg_ctr, (void*)g.atd_ln, (void*)g.ln_stats, (void*)g.hid_t,
-                    (void*)g.xkv_part, (void*)g.xkv_ctr})
+                    (void*)g.xkv_part, (void*)g.xkv_ctr, (void*)g.sa_part, (void*)g.sa_ctr})
       if (!p) return fail(WQ4_ENOMEM, "decode-group allocation failed");
     WA_HIP(hipMemset(g.xkv_ctr, 0, (size_t)kvc * c.n_text_head * sizeof(int)));
+    WA_HIP(hipMemset(g.sa_ctr, 0, (size_t)kvc * c.n_text_head * sizeof(int)));
     WA_HIP(hipMemset(g.atd_ln, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
     WA_HIP(hipMemset(g.hid_t, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));  // padded clips stay 0
     WA_HIP(hipMemset(g.lg_ctr, 0, sizeof(int)));
@@ -927,8 +933,13 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
                          wa::xattn_fused_q_supported((int)rows, Tq, D, m->wtype, m->ns);
     if (fuse_sa) {
       const wa::HeadProj hp{L.qkv_q16, L.qkv_d16, (int)L.proj_ku, g.atd_ln, g.ln_stats, L.qkv_wg, L.qkv_b2, D};
-      WA_HIP(wa::launch_decoder_self_attention_fused(hp, L.cache_k + self_ofs, L.cache_v + self_ofs, B, H,
-                                                     c.n_text_ctx, state, g.atd_dec, m->ns, st));
+      if (m->fuse_proj & kFuseSelfSplit)
+        WA_HIP(wa::launch_decoder_self_attention_split(hp, g.sa_part, g.sa_ctr, L.cache_k + self_ofs,
+                                                       L.cache_v + self_ofs, B, H, c.n_text_ctx, state, g.atd_dec,
+                                                       m->ns, st));
+      else
+        WA_HIP(wa::launch_decoder_self_attention_fused(hp, L.cache_k + self_ofs, L.cache_v + self_ofs, B, H,
+                                                       c.n_text_ctx, state, g.atd_dec, m->ns, st));
     } else {
       if (fold) {
         const wq4_ln_fold cons1{nullptr, nullptr, nullptr, g.ln_stats, L.qkv_wg};
@@ -1493,7 +1504,7 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
 int wa_model_wide_range(const wa_model* m) { return m ? (m->wide_range ? 1 : 0) : -1; }
 
 int wa_model_set_fused_projections(wa_model* m, int mask) {
-  if (!m || mask < -1 || mask > 3) return -1;
+  if (!m || mask < -1 || mask > 7) return -1;
   const int prev = m->fuse_proj;
   m->fuse_proj = mask < 0 ? kFuseDefault : mask;
   return prev;

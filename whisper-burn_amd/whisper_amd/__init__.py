@@ -301,7 +301,8 @@ class WhisperModel:
     def set_fused_projections(self, mask: int) -> int:
         """Diagnostics (wa_model_set_fused_projections): bit 0 the few-clip
         self-attention's q / k / v, bit 1 the cross-attention query formed
-        inside the attention launches; -1 = the product default.  Returns the
+        inside the attention launches, bit 2 (with bit 0) the self-attention's
+        projection spread over 8 workgroups per head; -1 = the product default.  Returns the
         previous mask."""
         prev = lib().wa_model_set_fused_projections(self._h, int(mask))
         if prev < 0:
