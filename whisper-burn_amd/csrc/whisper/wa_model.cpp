@@ -202,8 +202,11 @@ struct DecGroup {
 
 }  // namespace
 
-// the decode step's in-launch projections on by default (measured: DESIGN.md §4)
-constexpr int kFuseSelf = 1, kFuseCrossQ = 2, kFuseSelfSplit = 4, kFuseDefault = kFuseCrossQ;
+// The decode step's in-launch projections are off by default: the one-clip
+// A/B measured so far (self-attention per head + K / V cross-attention query,
+// profiles/r04c_fused_ab.json) was slower than the GEMM launches, and the
+// other forms are bit-identical but not yet timed.
+constexpr int kFuseSelf = 1, kFuseCrossQ = 2, kFuseSelfSplit = 4, kFuseDefault = 0;
 
 struct wa_model {
   int device = 0;
