@@ -351,7 +351,18 @@ def dry_run(args, rank: int, world: int) -> None:
     """`--dry-run`: the launch, rendezvous, barrier and max-over-ranks logic of
     a multi-rank run with no GPU work (the CPU test of `--gpus N`).  Each rank
     'runs' its clip shard (clip_ids) for a rank-dependent time; rank 0 prints
-    the one JSON line with n_gpus = world."""
+    the one JSON line with n_gpus = world.
+
+    Test-only fault injection: BENCH_DRY_RUN_FAIL="rank:status" makes that
+    rank print its PID and exit with `status` before the rendezvous, so the
+    other ranks block in it until launch_ranks stops them
+    (tests/test_bench_dist.py::test_bench_gpus_rank_failure_stops_the_others)."""
+    print(f"bench.py: rank {rank} pid {os.getpid()}", file=sys.stderr, flush=True)
+    fail = os.environ.get("BENCH_DRY_RUN_FAIL", "")
+    if fail:
+        fr, status = (int(v) for v in fail.split(":"))
+        if fr == rank:
+            sys.exit(status)
     dist = init_dist() if world > 1 else None
     ranks_seen = 1
     if dist is not None:
@@ -517,12 +528,15 @@ def main() -> None:
         q4 = prof["q4_gemm"]
         mean_tok = float(np.mean(ntok)) if ntok else 0.0
         steps_run = float(np.mean([t["steps"] for t in timings])) if timings else 0.0
-        # north-star kernel: the Q4 MFMA tile GEMMs of the encoder, timed live per launch
+        # north-star kernel: the encoder's Q4 MFMA GEMMs, timed live per launch;
+        # the kernel that ran them at this row count (tile or ring kernel)
+        enc_rows = B * cfg["n_audio_ctx"]
+        enc_kernel = wq4.gemm_kernel_name(cfg["n_audio_state"], cfg["n_audio_state"], enc_rows)
         q4_tf = q4["gflop"] / (q4["ms"] * 1e-3) * 1e-3 if q4["ms"] > 0 else 0.0
         roof_q4 = {"bound": "mfma", "achieved": round(q4_tf, 2), "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s",
                    "frac": round(q4_tf / PEAK_MFMA_TFLOPS, 4),
-                   "traffic": pmc_traffic("q4_gemm_prefill_kernel", workload),
-                   "kernel": "q4_gemm_prefill_kernel (encoder Q4 GEMMs)",
+                   "traffic": pmc_traffic(enc_kernel, workload),
+                   "kernel": f"{enc_kernel} (encoder Q4 GEMMs, M = {enc_rows})",
                    "launches": q4["launches"], "avg_us": round(q4["ms"] / max(1, q4["launches"]) * 1e3, 2),
                    "gpu_ms_per_step": round(q4["ms"] / args.steps, 2)}
         # decode phase: cross-attention (HBM stream of the encoder-output planes), probed after the timed steps

@@ -276,6 +276,11 @@ wq4_status wq4_quantize_q4_0(const float* x, int64_t n, uint8_t* out);
  * decode-step kernel (rows <= 32).  Each computes every output row with an
  * M-independent instruction sequence. */
 wq4_status wq4_set_kernel_policy(int policy);
+/* Name of the kernel a Q4_0 GEMM of `rows` rows over [n, k] weights runs
+ * under the current policy and encoder-kernel mode ("skinny_gemm_kernel",
+ * "q4_gemm_decode_kernel", "q4_gemm_enc_kernel", "q4_gemm_prefill_kernel";
+ * "" for a shape no GEMM accepts).  Host only (bench.py's roofline label). */
+const char* wq4_gemm_kernel_name(int64_t n, int64_t k, int64_t rows);
 
 /* ---- host-only diagnostics (no GPU needed) ---------------------------- */
 /* Sizes of the repacked nibble / scale / column-scale arrays for [N, K]. */

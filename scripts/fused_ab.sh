@@ -2,7 +2,7 @@
 # 0 none, 1 self-attention q/k/v (one workgroup per head), 2 cross-attention
 # query, 4 with 1: the self-attention projection over 8 workgroups per head
 set -o pipefail
-O=gpurun_out/${AB_OUT:-r04d}; mkdir -p $O; export TMPDIR=/tmp
+O=gpurun_out/${AB_OUT:-r05a}; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_fused_decode_gpu.py -x -v --timeout 300 --timeout-method thread > $O/fused.log 2>&1 || { grep -E "PASS|FAIL|Error" $O/fused.log | head -20; exit 1; }
 grep -cE "PASSED" $O/fused.log
 for F in 0 2 5 7 3; do

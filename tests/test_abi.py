@@ -138,6 +138,24 @@ def test_precision_and_policy_setters():
     wq4.set_kernel_policy(0)
 
 
+def test_gemm_kernel_name_follows_rows():
+    """wq4_gemm_kernel_name (bench.py's roofline label): the decode-step kernel
+    at <= 32 rows, the 8-wave decode kernel to 128, the encoder ring kernel at
+    one clip (M = 1500: the tile kernel's grid would leave CUs idle), the tile
+    kernel at 32 clips (M = 48000)."""
+    assert wq4.gemm_kernel_name(1280, 1280, 16) == "skinny_gemm_kernel"
+    assert wq4.gemm_kernel_name(1280, 1280, 100) == "q4_gemm_decode_kernel"
+    assert wq4.gemm_kernel_name(1280, 1280, 1500) == "q4_gemm_enc_kernel"
+    assert wq4.gemm_kernel_name(5120, 1280, 1500) == "q4_gemm_enc_kernel"
+    assert wq4.gemm_kernel_name(1280, 1280, 48000) == "q4_gemm_prefill_kernel"
+    assert wq4.gemm_kernel_name(1280, 1281, 16) == ""
+    wq4.set_kernel_policy(1)
+    try:
+        assert wq4.gemm_kernel_name(1280, 1280, 16) == "q4_gemm_prefill_kernel"
+    finally:
+        wq4.set_kernel_policy(0)
+
+
 def test_every_whisper_header_function_is_exported():
     import re
 

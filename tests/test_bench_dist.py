@@ -120,6 +120,30 @@ def test_bench_gpus_flag_launches_ranks():
     assert line["value"] == pytest.approx(2 * 4 * 2 * 30.0 / (line["ms_per_step"] * 2e-3), rel=1e-2)
 
 
+def test_bench_gpus_rank_failure_stops_the_others():
+    """One rank of `bench.py --gpus 2` exits with status 3 before the
+    rendezvous (test-only BENCH_DRY_RUN_FAIL): the other rank would wait in
+    init_process_group forever, so launch_ranks must terminate it and return
+    the failing rank's status."""
+    import re
+    import subprocess
+    import time
+
+    env = dict(_bench_env(), BENCH_DRY_RUN_FAIL="1:3")
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run"], env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 3, (out.returncode, out.stderr[-2000:])
+    assert "rank 1 exited with status 3" in out.stderr
+    assert time.time() - t0 < 200  # rank 0 was stopped, not left waiting for the rendezvous timeout
+    pids = {int(r): int(p) for r, p in re.findall(r"rank (\d) pid (\d+)", out.stderr)}
+    assert sorted(pids) == [0, 1]
+    for pid in pids.values():  # both children are gone (reaped by launch_ranks)
+        with pytest.raises(ProcessLookupError):
+            os.kill(pid, 0)
+    assert not any(s.startswith("{") for s in out.stdout.splitlines())  # no JSON line from a failed job
+
+
 def test_bench_one_gpu_dry_run_and_mismatch():
     import json
     import subprocess

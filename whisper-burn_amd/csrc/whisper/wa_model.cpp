@@ -137,6 +137,17 @@ struct Dev {
     ptrs.push_back(p);
     return static_cast<T*>(p);
   }
+  // frees one pointer alloc() returned (null: no-op)
+  void release(void* p) {
+    if (!p) return;
+    for (void*& q : ptrs)
+      if (q == p) {
+        (void)hipFree(q);
+        q = ptrs.back();
+        ptrs.pop_back();
+        return;
+      }
+  }
 };
 
 struct EncLayer {
@@ -207,6 +218,7 @@ struct DecGroup {
 // profiles/r04c_fused_ab.json) was slower than the GEMM launches, and the
 // other forms are bit-identical but not yet timed.
 constexpr int kFuseSelf = 1, kFuseCrossQ = 2, kFuseSelfSplit = 4, kFuseDefault = 0;
+constexpr int kFuseAll = kFuseSelf | kFuseCrossQ | kFuseSelfSplit;
 
 struct wa_model {
   int device = 0;
@@ -241,6 +253,7 @@ struct wa_model {
   // caches; a decode group entirely inside them reads the caches.
   int kv_clips = 0, kv_small = 0;
   int kv_n = 0;
+  bool kv_alloc_ok = false;  // every layer's xk / xv allocated (cross_kv_forward)
   bool group_kv(const DecGroup& g) const { return g.nb > 0 && g.b0 + g.nb <= kv_n; }
   hipStream_t own_stream = nullptr;  // encoder / encoder planes (graph capture needs a non-null stream)
   // Activation-range guard.  Every internal producer writes MFMA operands as
@@ -850,17 +863,31 @@ wq4_status cross_kv_forward(wa_model* m, int B, hipStream_t st, bool caches) {
   m->kv_batch = B;
   WA_HIP(wa::launch_enc_planes(m->enc_f32, rows, c.n_audio_state, m->ns, m->enc_planes, st));
   m->kv_n = caches && B <= m->kv_small ? B : 0;
-  if (m->kv_n > 0 && m->dec[0].xk == nullptr) {
+  if (m->kv_n > 0 && !m->kv_alloc_ok) {
+    // all layers or none: a partial failure frees what it got, so the next
+    // transcribe retries the allocation (or fails the same way) instead of
+    // running the cache GEMMs on a null layer
     const size_t n = (size_t)m->kv_clips * c.n_audio_ctx * c.n_text_state;
+    bool ok = true;
     for (DecLayer& L : m->dec) {
-      L.xk = m->dev.alloc<float>(n);
-      L.xv = m->dev.alloc<float>(n);
+      if (!L.xk) L.xk = m->dev.alloc<float>(n);
+      if (!L.xv) L.xv = m->dev.alloc<float>(n);
       if (!L.xk || !L.xv) {
-        m->kv_n = 0;
-        return fail(WQ4_ENOMEM, "cross K/V cache allocation failed");
+        ok = false;
+        break;
       }
-      m->bytes += n * 8;
     }
+    if (!ok) {
+      for (DecLayer& L : m->dec) {
+        m->dev.release(L.xk);
+        m->dev.release(L.xv);
+        L.xk = L.xv = nullptr;
+      }
+      m->kv_n = 0;
+      return fail(WQ4_ENOMEM, "cross K/V cache allocation failed");
+    }
+    m->bytes += n * 8 * m->dec.size();
+    m->kv_alloc_ok = true;
   }
   if (m->kv_n > 0) {
     // ln_post again, as the GEMMs' A-tiled operand (m->x still holds its
@@ -1087,9 +1114,11 @@ wq4_status prompt_group(wa_model* m, DecGroup& g, int lang_token, hipStream_t st
 wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
   // everything the captured step bakes in: the clip range (self-KV and
   // encoder-plane offsets), the EOT mode and the trace buffers
+  // buffers; one explicit field per mixed-radix digit
+  static_assert(kFuseAll < 8, "fuse_proj digit is 3 bits wide");
   const int64_t key =
-      (((((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0)) * 2 +
-       (m->group_kv(g) ? 1 : 0)) * 8 + (m->wide_range ? 1 : 0) + 2 * m->fuse_proj;
+      ((((((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0)) * 2 +
+        (m->group_kv(g) ? 1 : 0)) * 2 + (m->wide_range ? 1 : 0)) * 8 + (m->fuse_proj & kFuseAll);
   if (g.graph && g.graph_key == key) return WQ4_OK;
   if (g.graph) {
     (void)hipGraphExecDestroy(g.graph);

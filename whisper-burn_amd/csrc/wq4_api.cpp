@@ -255,6 +255,23 @@ wq4_status wq4_set_kernel_policy(int policy) {
   return WQ4_OK;
 }
 
+const char* wq4_gemm_kernel_name(int64_t n, int64_t k, int64_t rows) {
+  if (n < 1 || k < 32 || k % 32 != 0 || rows < 1) return "";
+  const wq4::Q4Geom g = wq4::make_geom(n, k);
+  // the decode-step layout exists for K % 128 == 0, N % 16 == 0 (upload)
+  const bool skinny = k % 128 == 0 && n % 16 == 0 && wq4::skinny_supported(g, (int)rows);
+  const int pol = g_policy.load();
+  int kern = pol != 0 ? (pol == 3 && !skinny ? 2 : pol) : skinny ? 3 : use_decode(rows) ? 2 : 1;
+  switch (kern) {
+    case 3: return "skinny_gemm_kernel";
+    case 2: return "q4_gemm_decode_kernel";
+    default:
+      return wq4::enc_gemm_pick(g, (int)rows, 0, g_prec.load() == WQ4_PREC_F16X2 ? 2 : 1, 0) != 0
+                 ? "q4_gemm_enc_kernel"
+                 : "q4_gemm_prefill_kernel";
+  }
+}
+
 // Q4Tensor::from_q4_bytes, src/gguf/tensor.rs:35-71.
 wq4_status wq4_tensor_create(int device, const uint8_t* raw, size_t nbytes, int64_t n, int64_t k,
                              wq4_tensor** out) {

@@ -53,6 +53,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.wq4_set_precision.argtypes = [c_int]
     L.wq4_get_precision.restype = c_int
     L.wq4_set_kernel_policy.argtypes = [c_int]
+    L.wq4_gemm_kernel_name.argtypes = [c_i64, c_i64, c_i64]
+    L.wq4_gemm_kernel_name.restype = ctypes.c_char_p
     L.wq4_tensor_create.argtypes = [c_int, u8p, c_sz, c_i64, c_i64, ctypes.POINTER(vp)]
     L.wq4_tensor_destroy.argtypes = [vp]
     L.wq4_tensor_destroy.restype = None
@@ -161,6 +163,12 @@ def set_kernel_policy(policy: int) -> None:
     """0 = automatic, 1 = MFMA tile ("prefill") kernel, 2 = K-split ("decode")
     kernel, 3 = decode-step kernel (include/wq4.h)."""
     check(lib().wq4_set_kernel_policy(policy))
+
+
+def gemm_kernel_name(n: int, k: int, rows: int) -> str:
+    """The kernel a Q4_0 GEMM of `rows` rows over [n, k] weights runs under the
+    current policy (host only; include/wq4.h wq4_gemm_kernel_name)."""
+    return lib().wq4_gemm_kernel_name(n, k, rows).decode()
 
 
 def _u8p(a: np.ndarray):
