@@ -411,9 +411,6 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--fused-proj", type=int, default=-1,
-                    help="diagnostics: mask of the decode-step projections formed inside the attention launches "
-                         "(1 self-attention q/k/v, 2 cross-attention query; -1 = the product default)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rendezvous / max-over-ranks only, no GPU work (CPU test of --gpus N)")
     args = ap.parse_args()
@@ -448,7 +445,6 @@ def main() -> None:
     model = whisper_amd.WhisperModel(args.variant, args.seed, max_batch=args.clips_per_gpu, device=local_rank,
                                      precision=prec, weights=args.weights)
     t_load = time.perf_counter() - t_load
-    model.set_fused_projections(args.fused_proj)
     cfg = model.config
     B = args.clips_per_gpu
     n_mels = cfg["n_mels"]
@@ -630,7 +626,6 @@ def main() -> None:
             "value_pcie_inclusive": round(job_rtf(world, B, args.steps, elapsed_pcie), 3),
             "log_mel_ms": round(float(np.mean(mel_ms)), 3) if mel_ms else None,
             "model_load_s": round(t_load, 2),
-            "fused_projections": args.fused_proj,
         }
         line["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline(model.config, args.cpu_rows, mean_tok)
         s = json.dumps(line)

@@ -104,14 +104,6 @@ wq4_status wq4_tensor_create_f16_ex(int device, const uint16_t* w, int64_t n, in
 int wq4_tensor_has_decode_step(const wq4_tensor* t);
 /* 0 = Q4_0 blocks, 1 = f16 weights. */
 int wq4_tensor_weight_type(const wq4_tensor* t);
-/* The decode-step layout of a Q4_0 tensor, for kernels of the model runtime
- * that form a projection inside their own launch (libwhisper_amd: the fused
- * decoder self-attention and cross-attention): q16 =
- * [N/16][ku][64 lanes][4 u32] nibbles, d16 = [N/16][ku][16 n][4] raw GGUF
- * f16 scales, ku = K/128 units of 4 blocks (wq4_skinny.hip).  Device
- * pointers owned by the tensor.  WQ4_EUNSUPPORTED if the tensor has none
- * (f16 weights, K % 128 != 0, N % 16 != 0, WQ4_TENSOR_NO_DECODE_STEP). */
-wq4_status wq4_tensor_decode_layout(const wq4_tensor* t, const uint32_t** q16, const uint16_t** d16, int64_t* ku);
 /* Q4Tensor::shape (tensor.rs:74-76): [N, K]. */
 wq4_status wq4_tensor_shape(const wq4_tensor* t, int64_t* n, int64_t* k);
 /* Q4Tensor::num_blocks (tensor.rs:79-81). */

@@ -10,8 +10,14 @@ to a GGUF and loaded by the product's loader; the oracle gets the same bytes):
     overflows; the model must notice (non-finite logits flag), re-run on the
     LayerNorm path (bounded operands) and return the f32 oracle's tokens.
   * "fc1": decoder layer 0's mlp.0 scaled by 5e3 -- fc1 outputs ~1e3-2e4, the
-    GELU output is fc2's operand: no bounded path exists, so transcribe must
-    FAIL LOUDLY (WQ4_ERANGE), never return tokens from NaN logits.
+    GELU output is fc2's operand and the LayerNorm path does not bound it:
+    the model must fall to range tier 2 (every FFN through the ABI's
+    per-call operand scales, wq4_ffn_forward_ws) and return the oracle's
+    tokens.
+  * "value": decoder layer 0's attn.value scaled by 3e5 -- the self-attention
+    output (a convex combination of values ~1e4) is the out projection's
+    operand, which no tier rescales: transcribe must FAIL LOUDLY
+    (WQ4_ERANGE), never return tokens from NaN logits.
 The oracle is float32 numpy (oracle/whisper_oracle.py) with a float64 run to
 check the fixture has no near-ties; it also records the activation
 magnitudes the fixture promises (CPU test below)."""
@@ -28,13 +34,15 @@ import whisper_oracle as wo
 SEED = 1234
 STEPS = 24
 CLIPS = (0, 1)
-SCALE = {"residual": 3.0e3, "fc1": 5.0e3}
+SCALE = {"residual": 3.0e3, "fc1": 5.0e3, "value": 3.0e5}
 
 
 def _scaled_names(kind: str) -> list[str]:
     if kind == "residual":
         return [f"decoder.blocks.{i}.{p}.{s}" for i in range(2) for p in ("attn.out", "cross_attn.out", "mlp.2")
                 for s in ("weight", "bias")]
+    if kind == "value":
+        return ["decoder.blocks.0.attn.value.weight", "decoder.blocks.0.attn.value.bias"]
     return ["decoder.blocks.0.mlp.0.weight", "decoder.blocks.0.mlp.0.bias"]
 
 
@@ -58,6 +66,7 @@ class _Recorder(wo.SynthWhisper):
     def __init__(self, *a, **k):
         self.max_resid = 0.0
         self.max_fc1 = 0.0
+        self.max_attn = 0.0  # self-attention outputs (the out projection's operand)
         super().__init__(*a, **k)
 
     def layer_norm(self, x, p):
@@ -66,6 +75,8 @@ class _Recorder(wo.SynthWhisper):
         return super().layer_norm(x, p)
 
     def linear(self, x, p, bias=True):
+        if p.startswith("decoder.blocks.") and p.endswith(".attn.out") and "cross" not in p:
+            self.max_attn = max(self.max_attn, float(np.max(np.abs(x))))
         y = super().linear(x, p, bias)
         if p.startswith("decoder.blocks.") and p.endswith("mlp.0"):
             self.max_fc1 = max(self.max_fc1, float(np.max(np.abs(y))))
@@ -101,23 +112,25 @@ def oracle_run(kind: str):
         t32 = m32.transcribe(mel, 50259, STEPS, eot_stop=False)
         m64 = stress_oracle(kind, np.float64)
         t64 = m64.transcribe(mel, 50259, STEPS, eot_stop=False)
-        _CACHE[kind] = (t32, t64, m32.max_resid, m32.max_fc1)
+        _CACHE[kind] = (t32, t64, m32.max_resid, m32.max_fc1, m32.max_attn)
     return _CACHE[kind]
 
 
-@pytest.mark.parametrize("kind", ["residual", "fc1"])
+@pytest.mark.parametrize("kind", ["residual", "fc1", "value"])
 def test_stress_fixture_reaches_the_range(kind):
     """CPU: the fixture really drives the activations to 1e3-2e4 (beyond the
     4094 the f16 pair of x * 2^4 holds), and the f32 oracle's tokens equal the
     f64 oracle's (no near-ties: the GPU comparison below is meaningful)."""
-    t32, t64, max_resid, max_fc1 = oracle_run(kind)
-    print(f"{kind}: max |residual| {max_resid:.4g}, max |fc1| {max_fc1:.4g}")
+    t32, t64, max_resid, max_fc1, max_attn = oracle_run(kind)
+    print(f"{kind}: max |residual| {max_resid:.4g}, max |fc1| {max_fc1:.4g}, max |attention| {max_attn:.4g}")
     assert t32 == t64
     if kind == "residual":
         assert 4094 < max_resid <= 2e4, max_resid
         assert max_fc1 < 100, max_fc1
-    else:
+    elif kind == "fc1":
         assert 4094 < max_fc1 <= 2e4, max_fc1
+    else:
+        assert max_attn > 4094, max_attn
 
 
 def _write(kind: str, tmp_path) -> str:
@@ -134,7 +147,7 @@ def test_residual_overflow_recovers_oracle_tokens(tmp_path):
 
     import whisper_amd
 
-    t32, _, _, _ = oracle_run("residual")
+    t32, _, _, _, _ = oracle_run("residual")
     m = whisper_amd.WhisperModel.from_gguf(_write("residual", tmp_path), "tiny_test", max_batch=len(CLIPS))
     assert not m.wide_range
     mel = torch.from_numpy(_mels(m.config["n_mels"])).cuda()
@@ -147,17 +160,40 @@ def test_residual_overflow_recovers_oracle_tokens(tmp_path):
 
 
 @pytest.mark.gpu
-def test_fc1_overflow_fails_loudly(tmp_path):
+def test_fc1_overflow_recovers_oracle_tokens(tmp_path):
+    """fc1 outputs beyond the f16 pair's range recover
+    through range tier 2 (per-call operand scales on every FFN) and give the
+    f32 oracle's tokens, as the reference's f32 path does."""
+    import torch
+
+    import whisper_amd
+
+    t32, _, _, _, _ = oracle_run("fc1")
+    m = whisper_amd.WhisperModel.from_gguf(_write("fc1", tmp_path), "tiny_test", max_batch=len(CLIPS))
+    mel = torch.from_numpy(_mels(m.config["n_mels"])).cuda()
+    toks = m.transcribe(mel, 50259, STEPS, eot_stop=False)
+    assert m.range_tier == 2
+    assert toks == t32
+    toks2 = m.transcribe(mel, 50259, STEPS, eot_stop=False)  # sticky: straight on tier 2
+    assert toks2 == t32 and m.range_tier == 2
+    m.close()
+
+
+@pytest.mark.gpu
+def test_value_overflow_fails_loudly(tmp_path):
+    """An attention output past the f16 pair's range (no tier rescales the out
+    projection's operand): WQ4_ERANGE after both retries, never NaN tokens."""
     import torch
 
     import whisper_amd
     import wq4
 
-    m = whisper_amd.WhisperModel.from_gguf(_write("fc1", tmp_path), "tiny_test", max_batch=len(CLIPS))
+    m = whisper_amd.WhisperModel.from_gguf(_write("value", tmp_path), "tiny_test", max_batch=len(CLIPS))
     mel = torch.from_numpy(_mels(m.config["n_mels"])).cuda()
     with pytest.raises(wq4.WQ4Error) as ei:
         m.transcribe(mel, 50259, STEPS, eot_stop=False)
     assert ei.value.status == 7 and "activation overflow" in ei.value.msg
+    assert m.range_tier == 2
     m.close()
 
 
@@ -171,5 +207,5 @@ def test_normal_model_never_flags():
     mel = torch.from_numpy(_mels(m.config["n_mels"])).cuda()
     m.transcribe(mel, 50259, STEPS, eot_stop=False)
     m.transcribe(mel, None, STEPS, eot_stop=True)
-    assert not m.wide_range
+    assert not m.wide_range and m.range_tier == 0
     m.close()

@@ -18,7 +18,6 @@
 
 #include "../wq4_device.hpp"
 #include "../wq4_lnmath.hpp"
-#include "wa_headproj.hpp"
 #include "wa_kernels.hpp"
 
 namespace wa {
@@ -355,7 +354,7 @@ hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Floa
 // 4-float K / V pointers of key j; vis(t, j) says whether query t sees key j.
 // attn_fetch issues one pass's loads (4 U keys per wave), attn_update folds
 // them in; attn_scan alternates the two.  A caller may issue the first pass's
-// loads itself before its queries exist (cross_attn_kv_kernel, FUSEQ).
+// loads itself before its queries exist.
 template <int TQ>
 __device__ __forceinline__ void attn_init(float (&m)[TQ], float (&l)[TQ], floatx4 (&o)[TQ]) {
 #pragma unroll
@@ -528,291 +527,6 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
   }
 }
 
-// s_waitcnt vmcnt(N), N a compile-time count (part of the instruction)
-template <int N>
-__device__ __forceinline__ void vmcnt_wait() {
-  static_assert(N == 0 || N == 16 || N == 24, "add the count");
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-}
-
-// Decode step (Tq = 1) of a few-clip group, Q4_0 weights: the self-attention
-// with its head's q / k / v formed inside the launch (decoder.rs:77-112,
-// attention.rs:93-125) -- one launch where the qkv GEMM + attention took two.
-// Workgroup (head, clip), 8 waves: the head's 12 column subtiles of the fused
-// qkv weight (q: 4 head, k: D/16 + 4 head, v: 2 D/16 + 4 head) and the clip's
-// A-tiled row of the LayerNorm fold (attn_ln) come into LDS by LDS-DMA
-// (wa_headproj.hpp; 149 KiB at D = 1280, one workgroup per CU), the eight
-// waves form the 192 values exactly as the decode-step GEMM would
-// (bit for bit), k / v are appended to the cache, and the keys are scanned
-// exactly as dec_self_attn_kernel scans them (this step's key from LDS).
-template <int NS>
-__global__ __launch_bounds__(512) void dec_self_attn_fused_kernel(HeadProj p, float* __restrict__ ck,
-                                                                  float* __restrict__ cv, int H, int ctx,
-                                                                  const DecodeState* __restrict__ state,
-                                                                  _Float16* __restrict__ tiled) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  __shared__ float wm[8][1], wl[8][1];
-  __shared__ float wo[8][1][64];
-  __shared__ __attribute__((aligned(16))) float qkv_s[3][64];
-  __shared__ float srow[2];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int head = blockIdx.x, b = blockIdx.y;
-  const int D = H * 64;
-  const int sub = lane & 15, grp = lane >> 4;
-  const int kv_len = state->kv_len;
-  const size_t hb = ((size_t)b * H + head) * ctx * 64;
-  auto sub_of = [&](int s) { return (s >> 2) * (D / 16) + 4 * head + (s & 3); };
-  hp_issue<1, 12>(p, sub_of, b, 1, smem, wave, 8, lane);
-  vmcnt_wait<0>();
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (wave == 0) {
-    float mean, den;
-    hp_row_stats<1, 12>(p, smem, 0, lane, mean, den);
-    if (lane == 0) {
-      srow[0] = mean;
-      srow[1] = den;
-    }
-  }
-  {
-    floatx4 acc[1][12];
-    hp_compute<1, 12, 1>(p, smem, wave, 8, lane, acc);
-    hp_store_red<1, 12, 1>(p, smem, wave, 8, lane, acc);
-  }
-  __syncthreads();
-  if (tid < 192) {
-    const float y = hp_finish<1, 12>(p, smem, 0, tid, srow[0], srow[1]);
-    const int part = tid >> 6, d = tid & 63;
-    qkv_s[part][d] = y;
-    // append k, v (decoder.rs:77-112 via Tensor::cat); read back from LDS below
-    if (part == 1) ck[hb + (size_t)kv_len * 64 + d] = y;
-    if (part == 2) cv[hb + (size_t)kv_len * 64 + d] = y;
-  }
-  __syncthreads();
-  // the scan of dec_self_attn_kernel (4 waves' key ranges, 8 keys in flight,
-  // the same merge: waves 4 .. 7 get empty ranges and merge as zeros), this
-  // step's key / value taken from LDS where that kernel reads the qkv rows
-  floatx4 qv[1];
-  qv[0] = *reinterpret_cast<const floatx4*>(&qkv_s[0][sub * 4]) * kEaQScale;
-  const floatx4 knew = *reinterpret_cast<const floatx4*>(&qkv_s[1][sub * 4]);
-  const floatx4 vnew = *reinterpret_cast<const floatx4*>(&qkv_s[2][sub * 4]);
-  const float* kb = ck + hb + sub * 4;
-  const float* vb = cv + hb + sub * 4;
-  const int nk = kv_len + 1;
-  const int per_wave = (nk + 3) / 4;
-  const int k0 = min(nk, wave * per_wave), k1 = min(nk, k0 + per_wave);
-  constexpr int U = 8;
-  float m[1], l[1];
-  floatx4 o[1];
-  attn_init<1>(m, l, o);
-  for (int j0 = k0; j0 < k1; j0 += 4 * U) {
-    floatx4 kk[U], vv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = max(0, min(j0 + 4 * u + grp, k1 - 1));
-      const int jc = max(0, min(j, kv_len - 1));  // cache rows only: loads never branch
-      const floatx4 kc = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(kb + (size_t)jc * 64));
-      const floatx4 vc = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(vb + (size_t)jc * 64));
-      kk[u] = j < kv_len ? kc : knew;
-      vv[u] = j < kv_len ? vc : vnew;
-    }
-    attn_update<1, U>(qv, 1, j0, k1, grp, [](int, int) { return true; }, kk, vv, m, l, o);
-  }
-  float mn, ls, os;
-  attn_merge<1, 8>(1, wave, lane, m, l, o, wm, wl, wo, mn, ls, os);
-  if (wave == 0) {
-    const float val = os / ls;
-    const float v1 = __shfl_down(val, 1, 64), v2 = __shfl_down(val, 2, 64), v3 = __shfl_down(val, 3, 64);
-    if ((lane & 3) == 0) atile_store4<NS>(tiled, b, head * 64 + lane, kbp_of(D), val, v1, v2, v3);
-  }
-}
-
-// The same step with the head's projection spread over 8 workgroups per
-// (head, clip) -- one per virtual wave of the decode-step GEMM's K split
-// (blocks [s kb / 8, (s + 1) kb / 8) of all 12 subtiles: ~29 KiB of LDS-DMA
-// per workgroup instead of 149 KiB in one, so 8x the CUs pull the weights).
-// Each publishes its 192 partial sums write-through (sc1) and takes a ticket;
-// the last arriver sums the 8 partials in split order (hp_finish's order),
-// applies the fold epilogue, appends k / v and runs dec_self_attn_kernel's
-// 4-wave scan.  Bit for bit the values of the qkv GEMM under kernel policy 3
-// followed by dec_self_attn_kernel.  part: [B][H][8][192] f32, ctr: [B][H]
-// tickets (zero; the last arriver re-arms its own).
-constexpr int kSaSplits = 8;
-__host__ __device__ constexpr int sa_split_lds_bytes(int ku) {
-  // W [12][2 units][64 pieces], D [12][2][8 pieces], A [<= 5 blocks][8 pieces]
-  return (12 * 2 * 64 + 12 * 2 * 8 + 64) * 16 + 0 * ku;
-}
-template <int NS>
-__global__ __launch_bounds__(256) void dec_self_attn_split_kernel(HeadProj p, float* __restrict__ part,
-                                                                  int* __restrict__ ctr, float* __restrict__ ck,
-                                                                  float* __restrict__ cv, int H, int ctx,
-                                                                  const DecodeState* __restrict__ state,
-                                                                  _Float16* __restrict__ tiled) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  __shared__ float wm[4][1], wl[4][1];
-  __shared__ float wo[4][1][64];
-  __shared__ __attribute__((aligned(16))) float qkv_s[3][64];
-  __shared__ float srow[2];
-  __shared__ int slast;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
-  const int D = H * 64, ku = p.ku, kb = 4 * ku;
-  const int b0 = (sp * kb) / kSaSplits, b1 = ((sp + 1) * kb) / kSaSplits;
-  const int u0 = b0 >> 2, nu = b1 > b0 ? ((b1 - 1) >> 2) - u0 + 1 : 0;  // units touched: <= 2 for K <= 1280
-  auto sub_of = [&](int s) { return (s >> 2) * (D / 16) + 4 * head + (s & 3); };
-  constexpr int kW = 0, kD = 12 * 2 * 64 * 16, kA = kD + 12 * 2 * 8 * 16;
-  constexpr uint32_t kOob = 0x7FFFFFF0u;
-  {  // LDS-DMA: 24 weight instructions (12 subtiles x 2 units), 3 of scales, 1 of activations
-    const __amdgpu_buffer_rsrc_t rw = hp_rsrc(p.q16, kOob);
-    const __amdgpu_buffer_rsrc_t rd = hp_rsrc(p.d16, kOob);
-    const __amdgpu_buffer_rsrc_t ra = hp_rsrc(p.at, (uint32_t)kb * 4u * 1024u);
-    for (int i = wave; i < 28; i += 4) {  // wave-uniform
-      if (i < 24) {
-        const int s = i >> 1, uu = i & 1;
-        const uint32_t off = uu < nu ? (uint32_t)((((size_t)sub_of(s) * ku + u0 + uu) * 64 + lane) * 16) : kOob;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (hp_lds_void*)(smem + kW + i * 1024), 16, off, 0, 0, 0);
-      } else if (i < 27) {
-        const int q = (i - 24) * 64 + lane, s = q >> 4, uu = (q >> 3) & 1, w8 = q & 7;
-        const uint32_t off = uu < nu ? (uint32_t)((((size_t)sub_of(s) * ku + u0 + uu) * 8 + w8) * 16) : kOob;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (hp_lds_void*)(smem + kD + (i - 24) * 1024), 16, off, 0, 0, 0);
-      } else {  // piece q: block b0 + q / 8, fragment ((b * 2 + kk) * 2 + plane), half q & 1 (row b of m-tile 0)
-        const int qa = b0 * 8 + lane, fr = qa >> 1, h = qa & 1;
-        const uint32_t off = lane < (b1 - b0) * 8 ? (uint32_t)((fr * 64 + b + 32 * h) * 16) : kOob;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (hp_lds_void*)(smem + kA), 16, off, 0, 0, 0);
-      }
-    }
-  }
-  vmcnt_wait<0>();
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  // wave w: subtiles w, w + 4, w + 8 over this split's blocks (hp_compute's
-  // per-virtual-wave chain: acc = fma(MFMA(x_hi, q) + MFMA(x_lo, q), d, acc))
-  const int r = lane & 15, g = lane >> 4;
-  floatx4 acc[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int bl = b0; bl < b1; ++bl) {
-    const int uu = (bl >> 2) - u0, bi = bl & 3;
-    wq4::half8 a[2];
-#pragma unroll
-    for (int pl = 0; pl < 2; ++pl) {
-      const int piece = (((bl * 2 + (g >> 1)) * 2 + pl) * 2 + (g & 1)) - b0 * 8;
-      const wq4::half8 x = *reinterpret_cast<const wq4::half8*>(smem + kA + piece * 16);
-      a[pl] = r != 0 ? wq4::half8{} : x;
-    }
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int s = wave + 4 * j, slot = s * 2 + uu;
-      const uint32_t w = *reinterpret_cast<const uint32_t*>(smem + kW + (slot * 64 + lane) * 16 + bi * 4);
-      const uint16_t dh = *reinterpret_cast<const uint16_t*>(smem + kD + (slot * 16 + r) * 8 + bi * 2);
-      const float d = (float)__builtin_bit_cast(_Float16, dh);
-      const wq4::half8 q = wq4::deq8(w);
-      floatx4 t = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], q, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      t = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], q, t, 0, 0, 0);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[j][e] = fmaf(t[e], d, acc[j][e]);
-    }
-  }
-  // publish row 0 (element 0 of lanes 0 .. 15) write-through, drain, ticket
-  const size_t ph = (size_t)b * H + head;
-  {
-    const __amdgpu_buffer_rsrc_t rp = hp_rsrc(part + (ph * kSaSplits + sp) * 192, 192 * 4);
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[j][0]), rp,
-                                              ((wave + 4 * j) * 16 + lane) * 4, 0, 16);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  typedef __attribute__((address_space(1))) int gint;
-  gint* tk = (gint*)(ctr + ph);
-  if (tid == 0) slast = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kSaSplits - 1;
-  __syncthreads();
-  if (!slast) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: the loads stay below the ticket
-  const int kv_len = state->kv_len;
-  const size_t hb = ph * ctx * 64;
-  if (wave == 0) {  // the row's LayerNorm statistics from the producer's tile statistics
-    const int tiles = p.K / 16, pt = lane & 15;
-    const float* st = p.stats + (size_t)b * tiles * 2;
-    wq4::floatx2 v[kHpLnPer];
-#pragma unroll
-    for (int u = 0; u < kHpLnPer; ++u) {
-      const int j = pt + 16 * u;
-      v[u] = j < tiles ? wq4::floatx2{st[2 * j], st[2 * j + 1]} : wq4::floatx2{0.0f, 0.0f};
-    }
-    float mean, den;
-    wq4::lnf_merge_tiles<kHpLnPer>(v, pt, tiles, mean, den);
-    if (lane == 0) {
-      srow[0] = mean;
-      srow[1] = den;
-    }
-  }
-  float y = 0.0f;
-  if (tid < 192) {
-    const __amdgpu_buffer_rsrc_t rp = hp_rsrc(part + ph * kSaSplits * 192, kSaSplits * 192 * 4);
-    float pv[kSaSplits];
-#pragma unroll
-    for (int s = 0; s < kSaSplits; ++s)
-      pv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, (s * 192 + tid) * 4, 0, 16));
-    y = pv[0];
-#pragma unroll
-    for (int s = 1; s < kSaSplits; ++s) y = y + pv[s];
-  }
-  const int col = sub_of(tid >> 4) * 16 + (tid & 15);
-  const float wg = tid < 192 ? p.wg[col] : 0.0f, bb = tid < 192 ? p.b2[col] : 0.0f;
-  __syncthreads();  // srow
-  if (tid < 192) {
-    y = wq4::lnf_apply(y * wq4::kActScaleInv, srow[0], wg, srow[1]) + bb;
-    const int pt = tid >> 6, d = tid & 63;
-    qkv_s[pt][d] = y;
-    if (pt == 1) ck[hb + (size_t)kv_len * 64 + d] = y;
-    if (pt == 2) cv[hb + (size_t)kv_len * 64 + d] = y;
-  }
-  if (tid == 0) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-  __syncthreads();
-  // dec_self_attn_kernel's scan: 4 waves' key ranges, 8 keys in flight, the
-  // new key / value from LDS
-  const int sub = lane & 15, grp = lane >> 4;
-  floatx4 qv[1];
-  qv[0] = *reinterpret_cast<const floatx4*>(&qkv_s[0][sub * 4]) * kEaQScale;
-  const floatx4 knew = *reinterpret_cast<const floatx4*>(&qkv_s[1][sub * 4]);
-  const floatx4 vnew = *reinterpret_cast<const floatx4*>(&qkv_s[2][sub * 4]);
-  const float* kbp = ck + hb + sub * 4;
-  const float* vbp = cv + hb + sub * 4;
-  const int nk = kv_len + 1;
-  const int per_wave = (nk + 3) / 4;
-  const int k0 = min(nk, wave * per_wave), k1 = min(nk, k0 + per_wave);
-  constexpr int U = 8;
-  float m[1], l[1];
-  floatx4 o[1];
-  attn_init<1>(m, l, o);
-  for (int j0 = k0; j0 < k1; j0 += 4 * U) {
-    floatx4 kk[U], vv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = max(0, min(j0 + 4 * u + grp, k1 - 1));
-      const int jc = max(0, min(j, kv_len - 1));  // cache rows only: loads never branch
-      const floatx4 kc = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(kbp + (size_t)jc * 64));
-      const floatx4 vc = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(vbp + (size_t)jc * 64));
-      kk[u] = j < kv_len ? kc : knew;
-      vv[u] = j < kv_len ? vc : vnew;
-    }
-    attn_update<1, U>(qv, 1, j0, k1, grp, [](int, int) { return true; }, kk, vv, m, l, o);
-  }
-  float mn, ls, os;
-  attn_merge<1, 4>(1, wave, lane, m, l, o, wm, wl, wo, mn, ls, os);
-  if (wave == 0) {
-    const float val = os / ls;
-    const float v1 = __shfl_down(val, 1, 64), v2 = __shfl_down(val, 2, 64), v3 = __shfl_down(val, 3, 64);
-    if ((lane & 3) == 0) atile_store4<NS>(tiled, b, head * 64 + lane, kbp_of(D), val, v1, v2, v3);
-  }
-}
-
 hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float* cache_v, int B, int Tq, int H,
                                          int ctx, const DecodeState* state, int kv_len_host, _Float16* tiled,
                                          int ns, hipStream_t st) {
@@ -827,33 +541,6 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
     if (Tq == 1) { WA_SELF(1, 1); } else { WA_SELF(1, 4); }
   }
 #undef WA_SELF
-  return hipGetLastError();
-}
-
-bool fused_proj_supported(int D, int ns) { return ns == 2 && hp_supported(1, 12, D) && hp_supported(1, 4, D); }
-
-hipError_t launch_decoder_self_attention_fused(const HeadProj& p, float* cache_k, float* cache_v, int B, int H, int ctx,
-                                               const DecodeState* state, _Float16* tiled, int ns, hipStream_t st) {
-  if (!state || ctx > kMaxCtx || H * 64 != p.K || !fused_proj_supported(p.K, ns) || !p.q16 || !p.d16 || !p.at ||
-      !p.stats || !p.wg || !p.b2 || p.ku * 128 != p.K)
-    return hipErrorInvalidValue;
-  const size_t lds = hp_lds_bytes(1, 12, p.ku);
-  hipLaunchKernelGGL((dec_self_attn_fused_kernel<2>), dim3(H, B), dim3(512), lds, st, p, cache_k, cache_v, H, ctx,
-                     state, tiled);
-  return hipGetLastError();
-}
-
-size_t self_attention_split_part_floats(int B, int H) { return (size_t)B * H * kSaSplits * 192; }
-
-hipError_t launch_decoder_self_attention_split(const HeadProj& p, float* part, int* ctr, float* cache_k,
-                                               float* cache_v, int B, int H, int ctx, const DecodeState* state,
-                                               _Float16* tiled, int ns, hipStream_t st) {
-  // the weights of one split span <= 2 units of 4 blocks: kb / 8 <= 5 (K <= 1280)
-  if (!state || !part || !ctr || ctx > kMaxCtx || H * 64 != p.K || !fused_proj_supported(p.K, ns) || !p.q16 ||
-      !p.d16 || !p.at || !p.stats || !p.wg || !p.b2 || p.ku * 128 != p.K || B < 1 || B > 32)
-    return hipErrorInvalidValue;
-  hipLaunchKernelGGL((dec_self_attn_split_kernel<2>), dim3(kSaSplits, H, B), dim3(256),
-                     (size_t)sa_split_lds_bytes(p.ku), st, p, part, ctr, cache_k, cache_v, H, ctx, state, tiled);
   return hipGetLastError();
 }
 
@@ -886,21 +573,13 @@ int cross_attention_kv_splits(int T) {
   return s < 1 ? 1 : (s > kXkvMaxSplit ? kXkvMaxSplit : s);
 }
 
-// FUSEQ (decode steps, Tq = 1, Q4_0 weights): the query projection runs
-// inside the launch -- the cq GEMM launch of the chain disappears.  Each
-// workgroup brings its head's 4 column subtiles of Wq (decode-step layout),
-// the clip's A-tiled cross_attn_ln fold row and the fold vectors into LDS by
-// LDS-DMA, issues its first pass of K / V loads behind them, and forms q of
-// its head with the decode-step GEMM's arithmetic (wa_headproj.hpp: the same
-// bits as that GEMM launch) while those loads fly.
-template <int NS, int TQ, bool FUSEQ>
+template <int NS, int TQ>
 __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restrict__ q, const float* __restrict__ kc,
                                                             const float* __restrict__ vc, int Tq_, int T, int H,
                                                             int S, float* __restrict__ part,
                                                             int* __restrict__ counters,
-                                                            _Float16* __restrict__ tiled, HeadProj fq) {
+                                                            _Float16* __restrict__ tiled) {
   constexpr int U = TQ == 1 ? 12 : 8;  // <= 48 keys per wave in flight at once (decode step)
-  static_assert(!FUSEQ || TQ == 1, "the fused query is a decode-step form");
   const int Tq = TQ == 1 ? 1 : Tq_;
   __shared__ float wm[4][TQ], wl[4][TQ];
   __shared__ float wo[4][TQ][64];
@@ -924,46 +603,12 @@ __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restr
   floatx4 o[TQ];
   floatx4 qv[TQ];
   attn_init<TQ>(m, l, o);
-  int j0 = k0;
-  if constexpr (FUSEQ) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ float qs[64];
-    __shared__ float srow[2];
-    hp_issue<1, 4>(fq, [&](int s) { return 4 * head + s; }, b, 1, smem, wave, 4, lane);
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    floatx4 kk[U], vv[U];  // the first pass of K / V, in flight behind the LDS-DMA
-    attn_fetch<U>(j0, k1, grp, rows, kk, vv);
-    vmcnt_wait<2 * U>();   // every DMA piece has landed; the 2U younger K / V loads may still fly
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (wave == 0) {
-      float mean, den;
-      hp_row_stats<1, 4>(fq, smem, 0, lane, mean, den);
-      if (lane == 0) {
-        srow[0] = mean;
-        srow[1] = den;
-      }
-    }
-    {
-      floatx4 acc[2][4];
-      hp_compute<1, 4, 2>(fq, smem, wave, 4, lane, acc);
-      hp_store_red<1, 4, 2>(fq, smem, wave, 4, lane, acc);
-    }
-    __syncthreads();
-    if (tid < 64) qs[tid] = hp_finish<1, 4>(fq, smem, 0, tid, srow[0], srow[1]);
-    __syncthreads();
-    qv[0] = *reinterpret_cast<const floatx4*>(&qs[sub * 4]) * kEaQScale;
-    if (j0 < k1) attn_update<TQ, U>(qv, Tq, j0, k1, grp, [](int, int) { return true; }, kk, vv, m, l, o);
-    j0 += 4 * U;
-  } else {
 #pragma unroll
-    for (int t = 0; t < TQ; ++t)
-      qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(q + (size_t)(b * Tq + t) * D + head * 64 + sub * 4) *
-                           kEaQScale
-                     : floatx4{0.f, 0.f, 0.f, 0.f};
-  }
-  for (; j0 < k1; j0 += 4 * U) {
+  for (int t = 0; t < TQ; ++t)
+    qv[t] = t < Tq ? *reinterpret_cast<const floatx4*>(q + (size_t)(b * Tq + t) * D + head * 64 + sub * 4) *
+                         kEaQScale
+                   : floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int j0 = k0; j0 < k1; j0 += 4 * U) {
     floatx4 kk[U], vv[U];
     attn_fetch<U>(j0, k1, grp, rows, kk, vv);
     attn_update<TQ, U>(qv, Tq, j0, k1, grp, [](int, int) { return true; }, kk, vv, m, l, o);
@@ -1029,25 +674,17 @@ size_t cross_attention_kv_part_floats(int B, int H, int T) {
 }
 
 hipError_t launch_cross_attention_kv(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
-                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st,
-                                     const HeadProj* fuse) {
-  if (Tq < 1 || Tq > 4 || B < 1 || T < 1 || H < 1) return hipErrorInvalidValue;
-  if (fuse && (Tq != 1 || H * 64 != fuse->K || !fused_proj_supported(fuse->K, ns) || fuse->ku * 128 != fuse->K ||
-               !fuse->q16 || !fuse->d16 || !fuse->at || !fuse->stats || !fuse->wg || !fuse->b2))
-    return hipErrorInvalidValue;
-  if (!fuse && !q) return hipErrorInvalidValue;
-  const HeadProj fq = fuse ? *fuse : HeadProj{};
+                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st) {
+  if (Tq < 1 || Tq > 4 || B < 1 || T < 1 || H < 1 || !q) return hipErrorInvalidValue;
   const int S = cross_attention_kv_splits(T);
   const dim3 grid(H * S, B), block(256);
-#define WA_XKV(NS_, TQ_, F_, LDS_)                                                                              \
-  hipLaunchKernelGGL((cross_attn_kv_kernel<NS_, TQ_, F_>), grid, block, LDS_, st, q, k, v, Tq, T, H, S, part, \
-                     counters, tiled, fq)
-  if (fuse) {
-    WA_XKV(2, 1, true, (size_t)hp_lds_bytes(1, 4, fuse->ku));
-  } else if (ns == 2) {
-    if (Tq == 1) { WA_XKV(2, 1, false, 0); } else { WA_XKV(2, 4, false, 0); }
+#define WA_XKV(NS_, TQ_)                                                                                           \
+  hipLaunchKernelGGL((cross_attn_kv_kernel<NS_, TQ_>), grid, block, 0, st, q, k, v, Tq, T, H, S, part, counters, \
+                     tiled)
+  if (ns == 2) {
+    if (Tq == 1) { WA_XKV(2, 1); } else { WA_XKV(2, 4); }
   } else {
-    if (Tq == 1) { WA_XKV(1, 1, false, 0); } else { WA_XKV(1, 4, false, 0); }
+    if (Tq == 1) { WA_XKV(1, 1); } else { WA_XKV(1, 4); }
   }
 #undef WA_XKV
   return hipGetLastError();

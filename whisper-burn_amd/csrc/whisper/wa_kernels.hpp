@@ -30,48 +30,16 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
                                          int ctx, const DecodeState* state, int kv_len_host, _Float16* tiled,
                                          int ns, hipStream_t st);
 
-// In-launch projections of a few-clip decode step (wa_headproj.hpp): the
-// projection's decode-step weight layout + the LayerNorm-fold operand it
-// reads.  Supported for f16x2 operands (ns == 2), D % 256 == 0, D <= 1280.
-struct HeadProj {
-  const uint32_t* q16;  // decode-step nibbles of the weight (wq4_tensor_decode_layout)
-  const uint16_t* d16;  //   its f16 block scales
-  int ku;               // units of 4 Q4 blocks per 16-column subtile (K / 128)
-  const _Float16* at;   // A-tiled f16-pair operand of the rows: the LayerNorm-fold x * gamma (m-tile 0)
-  const float* stats;   // the fold producer's (mean, M2) per (row, 16-column tile) [rows][K / 16][2]
-  const float* wg;      // W gamma [N]
-  const float* b2;      // W beta + bias [N]
-  int K;                // input width (= n_text_state)
-};
-bool fused_proj_supported(int D, int ns);
-// The decode step's (Tq = 1) self-attention with its head's q / k / v formed
-// in the launch from the fused qkv weight (p: N = 3D, the attn_ln fold) --
-// the qkv GEMM launch and this attention in one launch, the same bits.
-hipError_t launch_decoder_self_attention_fused(const HeadProj& p, float* cache_k, float* cache_v, int B, int H, int ctx,
-                                               const DecodeState* state, _Float16* tiled, int ns, hipStream_t st);
-// The same, the projection spread over 8 workgroups per (head, clip) (the
-// decode-step GEMM's K split) whose last arriver finishes it and runs the
-// attention; part: self_attention_split_part_floats floats, ctr: B * H ints
-// zeroed once (re-armed by the kernel).  The same bits.
-size_t self_attention_split_part_floats(int B, int H);
-hipError_t launch_decoder_self_attention_split(const HeadProj& p, float* part, int* ctr, float* cache_k,
-                                               float* cache_v, int B, int H, int ctx, const DecodeState* state,
-                                               _Float16* tiled, int ns, hipStream_t st);
-
 // Cross-attention over cached K / V (attention.rs:177-236, the reference's
 // form; used for decode groups of a few clips): q [B*Tq, D] f32, k / v
 // head-major [B][H][T][64] f32 (wq4_gemm_tiled_headmajor of the encoder
 // output), Tq <= 4; part: cross_attention_kv_part_floats floats, counters:
 // B * H ints zeroed once (re-armed by the kernel).  Writes the A-tiled
 // operand of the output projection.
-// With fuse != nullptr (Tq = 1) q is not read: each workgroup forms its
-// head's query from the cq weight (the cross_attn_ln fold, wa_headproj.hpp),
-// the same bits as the cq GEMM launch it replaces.
 int cross_attention_kv_splits(int T);
 size_t cross_attention_kv_part_floats(int B, int H, int T);
 hipError_t launch_cross_attention_kv(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
-                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st,
-                                     const HeadProj* fuse = nullptr);
+                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st);
 
 // Cross-attention over the encoder output (wa_xattn.hip; attention.rs:
 // 204-298 restated without K/V caches): q [B*Tq, D] f32 (rows b*Tq + i),
@@ -91,14 +59,9 @@ size_t xattn_part_floats(int R, int H, int D, int T);
 size_t wv_pack_words(int H, int D);
 hipError_t launch_wv_pack(const uint8_t* wv, int H, int D, uint32_t* out, hipStream_t st);
 // wvp: the launch_wv_pack words of wv (Q4 weights; ignored for f16 weights).
-// With fuse != nullptr (decode steps of <= 16 clips, Q4_0, f16x2:
-// xattn_fused_q_supported) q is not read: the query transform forms each
-// head's query from the cq weight (the cross_attn_ln fold) in the same
-// launch -- the same bits as the cq GEMM under kernel policy 3.
-bool xattn_fused_q_supported(int R, int Tq, int D, int wtype, int ns);
 hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, const uint32_t* wvp, const float* bv,
                         int wtype, const _Float16* enc, int B, int Tq, int T, int H, int D, _Float16* qt, float* part,
-                        _Float16* tiled, int ns, hipStream_t st, const HeadProj* fuse = nullptr);
+                        _Float16* tiled, int ns, hipStream_t st);
 // A-tiled operand [R][K] (hi + lo) -> f32 rows (diagnostics).
 hipError_t launch_untile(const _Float16* tiled, int R, int K, int ns, float* out, hipStream_t st);
 // f32 rows [rows][D] -> [rows][ns][D] f16 planes (hi | lo) for launch_xattn.

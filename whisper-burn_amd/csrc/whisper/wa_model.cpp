@@ -166,11 +166,6 @@ struct DecLayer {
   // cross-attention key / value weights in raw GGUF form (Q4_0 blocks or
   // f16), read by the K/V-cache-free cross-attention (wa_xattn.hip)
   uint8_t *ck_raw = nullptr, *cv_raw = nullptr;
-  // decode-step layouts of qkv and cq (wq4_tensor_decode_layout) for the
-  // in-launch projections of few-clip decode steps (wa_headproj.hpp)
-  const uint32_t *qkv_q16 = nullptr, *cq_q16 = nullptr;
-  const uint16_t *qkv_d16 = nullptr, *cq_d16 = nullptr;
-  int64_t proj_ku = 0;
   uint32_t* cv_p = nullptr;  // Q4_0: cv_raw in the projection's lane order (wa::launch_wv_pack)
   float *cache_k, *cache_v;
   // few-clip decode groups (wa_model::kv_clips): the reference's per-layer
@@ -198,14 +193,14 @@ struct DecGroup {
   float* xattn_part;  // cross-attention split partials (Z, max, sum)
   float* xkv_part;    // cross-attention over cached K / V: split partials
   int* xkv_ctr;       //   and the per-(clip, head) arrival counters
-  float* sa_part;     // split self-attention (dec_self_attn_split_kernel): partials
-  int* sa_ctr;        //   and the per-(clip, head) arrival counters
   _Float16* atd_ln;   // LayerNorm fold: A-tiled x * gamma of the next LayerNorm
   float* ln_stats;    //                 its per (row, 32-column tile) mean / M2
   _Float16* hid_t;    // fused logits + argmax: the final LN, A-tiled (m-tile 0)
   float* lg_val;      //                        per-workgroup candidates [32][groups]
   int *lg_idx, *lg_ctr;
   wa::DecodeState* state;
+  void* ffn_ws = nullptr;  // wide_ffn: wq4_ffn_forward_ws workspace (4 * nb rows)
+  size_t ffn_ws_bytes = 0;
   int* host_ndone = nullptr;  // pinned ring
   hipGraphExec_t graph = nullptr;
   int64_t graph_key = -1;  // (b0, nb, eot mode, trace) the graph was captured for
@@ -213,12 +208,6 @@ struct DecGroup {
 
 }  // namespace
 
-// The decode step's in-launch projections are off by default: the one-clip
-// A/B measured so far (self-attention per head + K / V cross-attention query,
-// profiles/r04c_fused_ab.json) was slower than the GEMM launches, and the
-// other forms are bit-identical but not yet timed.
-constexpr int kFuseSelf = 1, kFuseCrossQ = 2, kFuseSelfSplit = 4, kFuseDefault = 0;
-constexpr int kFuseAll = kFuseSelf | kFuseCrossQ | kFuseSelfSplit;
 
 struct wa_model {
   int device = 0;
@@ -266,13 +255,15 @@ struct wa_model {
   // |beta|); still flagged -> WQ4_ERANGE, never NaN tokens.
   int* range_flag = nullptr;
   bool wide_range = false;
-  // decode steps form projections inside the attention launches
-  // (wa_headproj.hpp): bit 0 the few-clip self-attention's q / k / v (bit 2:
-  // spread over 8 workgroups per head, dec_self_attn_split_kernel), bit 1
-  // the cross-attention query (few-clip K / V form and <= 16-clip groups on
-  // the encoder planes); wa_model_set_fused_projections (diagnostics, the
-  // bit-equality test)
-  int fuse_proj = kFuseDefault;
+  // second tier (wide_range still flagged): the encoder and decoder FFNs run
+  // as Q4FFN::forward at the ABI (wq4_ffn_forward_ws: LayerNorm output in
+  // f32, fc1 + GELU to f32, each GEMM operand scaled by a power of two picked
+  // per call from its max |x|), so fc1 / GELU outputs of any f32-finite size
+  // reach fc2 finite.  Workspaces allocated when the tier is entered:
+  // ffn_ws for the encoder's B * T rows, g.ffn_ws per decode group.
+  bool wide_ffn = false;
+  void* ffn_ws = nullptr;
+  size_t ffn_ws_bytes = 0;
   float timings[5] = {0, 0, 0, 0, 0};
   // decode-step logit trace (wa_transcribe_trace; null otherwise): device
   // [clip][trace_s1][trace_k] ids and their logits
@@ -600,12 +591,6 @@ wq4_status build_model(wa_model* m, Source& src) {
     L.fc2 = B.q4({p + ".mlp.2.weight"}, {Dt}, Ft);
     L.fc2_b = B.vec(p + ".mlp.2.bias", Dt, -0.02f, 0.02f);
     if (B.st != WQ4_OK) return B.st;
-    if (m->wtype == 0) {  // Q4_0: the few-clip decode step's in-launch projections read these
-      int64_t ku2 = 0;
-      if (wq4_tensor_decode_layout(L.qkv, &L.qkv_q16, &L.qkv_d16, &L.proj_ku) != WQ4_OK ||
-          wq4_tensor_decode_layout(L.cq, &L.cq_q16, &L.cq_d16, &ku2) != WQ4_OK || ku2 != L.proj_ku)
-        L.qkv_q16 = L.cq_q16 = nullptr;
-    }
   }
   m->dln_w = B.vec("decoder.ln.weight", Dt, 0.9f, 1.1f);
   m->dln_b = B.vec("decoder.ln.bias", Dt, -0.05f, 0.05f);
@@ -719,8 +704,6 @@ wq4_status alloc_activations(wa_model* m) {
     const int kvc = std::max(1, m->kv_clips);
     g.xkv_part = f32((int64_t)wa::cross_attention_kv_part_floats(kvc, c.n_text_head, T));
     g.xkv_ctr = d.alloc<int>((size_t)kvc * c.n_text_head);
-    g.sa_part = f32((int64_t)wa::self_attention_split_part_floats(kvc, c.n_text_head));
-    g.sa_ctr = d.alloc<int>((size_t)kvc * c.n_text_head);
     g.xqt = d.alloc<_Float16>((size_t)rdec * m->ns * HP * Dt);
     g.atd_ln = tiled(rdec, Dt);
     g.ln_stats = f32(rdec * (Dt / 16) * 2);  // per 16-column tile (the decode-step GEMM)
@@ -733,10 +716,9 @@ wq4_status alloc_activations(wa_model* m) {
                     (void*)g.atf_dec, (void*)g.prompt_tok, (void*)g.next_tok, (void*)g.tokens, (void*)g.ntok,
                     (void*)g.done, (void*)g.state, (void*)g.xattn_part, (void*)g.xqt, (void*)g.lg_val,
                     (void*)g.lg_idx, (void*)g.lg_ctr, (void*)g.atd_ln, (void*)g.ln_stats, (void*)g.hid_t,
-                    (void*)g.xkv_part, (void*)g.xkv_ctr, (void*)g.sa_part, (void*)g.sa_ctr})
+                    (void*)g.xkv_part, (void*)g.xkv_ctr})
       if (!p) return fail(WQ4_ENOMEM, "decode-group allocation failed");
     WA_HIP(hipMemset(g.xkv_ctr, 0, (size_t)kvc * c.n_text_head * sizeof(int)));
-    WA_HIP(hipMemset(g.sa_ctr, 0, (size_t)kvc * c.n_text_head * sizeof(int)));
     WA_HIP(hipMemset(g.atd_ln, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
     WA_HIP(hipMemset(g.hid_t, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));  // padded clips stay 0
     WA_HIP(hipMemset(g.lg_ctr, 0, sizeof(int)));
@@ -822,6 +804,12 @@ wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st,
     {
       Prof p = q4prof(m, st, L.out, rows);
       WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, m->at_d, m->x, m->x, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 1, st));
+    }
+    if (m->wide_ffn) {  // range tier 2: Q4FFN::forward with per-call operand scales (m->qkv: f32 scratch)
+      WA_WQ4(wq4_layernorm(m->x, L.ln2_w, L.ln2_b, rows, D, WQ4_PREC_F16X2, nullptr, m->qkv, st));
+      WA_WQ4(wq4_ffn_forward_ws(L.fc1, L.fc1_b, L.fc2, L.fc2_b, m->qkv, m->x, m->x, rows, WQ4_EPI_RESIDUAL, m->prec,
+                                m->ffn_ws, m->ffn_ws_bytes, st));
+      continue;
     }
     {
       Prof p(m, st, 3, 0.0, ln_gb);
@@ -949,60 +937,34 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
   const int nl = (int)m->dec.size();
   for (int li = 0; li < nl; ++li) {  // DecoderBlock (decoder.rs:77-112 / 140-183)
     DecLayer& L = m->dec[li];
-    // few-clip decode steps (Q4_0, f16x2): the self-attention forms its head's
-    // q / k / v and the K / V cross-attention its query inside their own
-    // launches from the LayerNorm-fold operand (wa_headproj.hpp) -- the qkv
-    // and cq GEMM launches leave the chain, the values are the same bits
-    const bool proj = fold && L.qkv_q16 != nullptr && L.cq_q16 != nullptr;
-    const bool kvf = proj && m->group_kv(g) && wa::fused_proj_supported(D, m->ns);
-    const bool fuse_sa = kvf && (m->fuse_proj & kFuseSelf);
-    const bool fuse = kvf && (m->fuse_proj & kFuseCrossQ);  // the K / V cross-attention's query
-    // groups of <= 16 clips streaming the encoder planes: the cross-attention
-    // query transform forms the query itself (xattn_q_fused_kernel)
-    const bool fuse_xq = proj && (m->fuse_proj & kFuseCrossQ) && !m->group_kv(g) &&
-                         wa::xattn_fused_q_supported((int)rows, Tq, D, m->wtype, m->ns);
-    if (fuse_sa) {
-      const wa::HeadProj hp{L.qkv_q16, L.qkv_d16, (int)L.proj_ku, g.atd_ln, g.ln_stats, L.qkv_wg, L.qkv_b2, D};
-      if (m->fuse_proj & kFuseSelfSplit)
-        WA_HIP(wa::launch_decoder_self_attention_split(hp, g.sa_part, g.sa_ctr, L.cache_k + self_ofs,
-                                                       L.cache_v + self_ofs, B, H, c.n_text_ctx, state, g.atd_dec,
-                                                       m->ns, st));
-      else
-        WA_HIP(wa::launch_decoder_self_attention_fused(hp, L.cache_k + self_ofs, L.cache_v + self_ofs, B, H,
-                                                       c.n_text_ctx, state, g.atd_dec, m->ns, st));
+    if (fold) {
+      const wq4_ln_fold cons1{nullptr, nullptr, nullptr, g.ln_stats, L.qkv_wg};
+      WA_WQ4(wq4_gemm_tiled_lnfold(L.qkv, L.qkv_b2, g.atd_ln, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, &cons1,
+                                   st));
     } else {
-      if (fold) {
-        const wq4_ln_fold cons1{nullptr, nullptr, nullptr, g.ln_stats, L.qkv_wg};
-        WA_WQ4(wq4_gemm_tiled_lnfold(L.qkv, L.qkv_b2, g.atd_ln, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, &cons1,
-                                     st));
-      } else {
-        WA_WQ4(wq4_layernorm(g.xd, L.ln1_w, L.ln1_b, rows, D, m->prec, g.atd_dec, nullptr, st));
-        WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, g.atd_dec, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, 2, st));
-      }
-      WA_HIP(wa::launch_decoder_self_attention(g.qkvd, L.cache_k + self_ofs, L.cache_v + self_ofs, B, Tq, H,
-                                               c.n_text_ctx, state, kv0, g.atd_dec, m->ns, st));
+      WA_WQ4(wq4_layernorm(g.xd, L.ln1_w, L.ln1_b, rows, D, m->prec, g.atd_dec, nullptr, st));
+      WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, g.atd_dec, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, 2, st));
     }
+    WA_HIP(wa::launch_decoder_self_attention(g.qkvd, L.cache_k + self_ofs, L.cache_v + self_ofs, B, Tq, H,
+                                             c.n_text_ctx, state, kv0, g.atd_dec, m->ns, st));
     if (fold) {
       const wq4_ln_fold prod2{L.ln2_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
       WA_WQ4(wq4_gemm_tiled_lnfold(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec,
                                    &prod2, st));
-      if (!fuse && !fuse_xq) {
-        const wq4_ln_fold cons2{nullptr, nullptr, nullptr, g.ln_stats, L.cq_wg};
-        WA_WQ4(wq4_gemm_tiled_lnfold(L.cq, L.cq_b2, g.atd_ln, nullptr, g.qd, nullptr, rows, 0u, m->prec, &cons2, st));
-      }
+      const wq4_ln_fold cons2{nullptr, nullptr, nullptr, g.ln_stats, L.cq_wg};
+      WA_WQ4(wq4_gemm_tiled_lnfold(L.cq, L.cq_b2, g.atd_ln, nullptr, g.qd, nullptr, rows, 0u, m->prec, &cons2, st));
     } else {
       WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2, st));
       WA_WQ4(wq4_layernorm(g.xd, L.ln2_w, L.ln2_b, rows, D, m->prec, g.atd_dec, nullptr, st));
       WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, g.atd_dec, nullptr, g.qd, nullptr, rows, 0u, m->prec, 2, st));
     }
-    const wa::HeadProj hq{L.cq_q16, L.cq_d16, (int)L.proj_ku, g.atd_ln, g.ln_stats, L.cq_wg, L.cq_b2, D};
     if (m->group_kv(g)) {  // few clips: one GEMV launch over the cached K / V
       const size_t kofs = (size_t)g.b0 * T * D;
-      WA_HIP(wa::launch_cross_attention_kv(fuse ? nullptr : g.qd, L.xk + kofs, L.xv + kofs, B, Tq, T, H, g.xkv_part,
-                                           g.xkv_ctr, g.atd_dec, m->ns, st, fuse ? &hq : nullptr));
+      WA_HIP(wa::launch_cross_attention_kv(g.qd, L.xk + kofs, L.xv + kofs, B, Tq, T, H, g.xkv_part, g.xkv_ctr,
+                                           g.atd_dec, m->ns, st));
     } else {
-      WA_HIP(wa::launch_xattn(fuse_xq ? nullptr : g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, Tq, T, H,
-                              D, g.xqt, g.xattn_part, g.atd_dec, m->ns, st, fuse_xq ? &hq : nullptr));
+      WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, Tq, T, H, D, g.xqt,
+                              g.xattn_part, g.atd_dec, m->ns, st));
     }
     if (fold) {
       const wq4_ln_fold prod3{L.ln3_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
@@ -1020,6 +982,12 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
     } else {
       WA_WQ4(wq4_gemm_tiled(L.cout, L.cout_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2,
                             st));
+      if (m->wide_ffn) {  // range tier 2: Q4FFN::forward with per-call operand scales (g.hid: f32 scratch)
+        WA_WQ4(wq4_layernorm(g.xd, L.ln3_w, L.ln3_b, rows, D, WQ4_PREC_F16X2, nullptr, g.hid, st));
+        WA_WQ4(wq4_ffn_forward_ws(L.fc1, L.fc1_b, L.fc2, L.fc2_b, g.hid, g.xd, g.xd, rows, WQ4_EPI_RESIDUAL,
+                                  m->prec, g.ffn_ws, g.ffn_ws_bytes, st));
+        continue;
+      }
       WA_WQ4(wq4_layernorm(g.xd, L.ln3_w, L.ln3_b, rows, D, m->prec, g.atd_dec, nullptr, st));
       WA_WQ4(wq4_gemm_tiled(L.fc1, L.fc1_b, g.atd_dec, nullptr, nullptr, g.atf_dec, rows,
                             WQ4_EPI_GELU | WQ4_EPI_TILED_OUT, m->prec, 2, st));
@@ -1114,11 +1082,10 @@ wq4_status prompt_group(wa_model* m, DecGroup& g, int lang_token, hipStream_t st
 wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
   // everything the captured step bakes in: the clip range (self-KV and
   // encoder-plane offsets), the EOT mode and the trace buffers
-  // buffers; one explicit field per mixed-radix digit
-  static_assert(kFuseAll < 8, "fuse_proj digit is 3 bits wide");
+  // buffers, the range tier; one explicit field per mixed-radix digit
   const int64_t key =
-      ((((((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0)) * 2 +
-        (m->group_kv(g) ? 1 : 0)) * 2 + (m->wide_range ? 1 : 0)) * 8 + (m->fuse_proj & kFuseAll);
+      (((((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0)) * 2 +
+       (m->group_kv(g) ? 1 : 0)) * 3 + (m->wide_ffn ? 2 : m->wide_range ? 1 : 0);
   if (g.graph && g.graph_key == key) return WQ4_OK;
   if (g.graph) {
     (void)hipGraphExecDestroy(g.graph);
@@ -1147,6 +1114,29 @@ void kv_config(wa_model* m, int max_batch) {
   }();
   m->kv_small = std::min(small, max_batch);
   m->kv_clips = m->kv_small;
+}
+
+// Range tier 2's workspaces (wq4_ffn_forward_ws): the encoder's B * T rows
+// and 4 * B rows per decode group (prompts), allocated once.
+wq4_status ensure_ffn_ws(wa_model* m) {
+  if (m->ffn_ws) return WQ4_OK;
+  const DecLayer& Ld = m->dec.front();
+  const EncLayer& Le = m->enc.front();
+  const size_t ne = wq4_ffn_workspace_bytes(Le.fc1, Le.fc2, (int64_t)m->bmax * m->cfg.n_audio_ctx);
+  const size_t nd = wq4_ffn_workspace_bytes(Ld.fc1, Ld.fc2, (int64_t)m->bmax * 4);
+  if (ne == 0 || nd == 0) return fail(WQ4_EINVAL, "FFN workspace size");
+  void* e = m->dev.alloc<uint8_t>(ne);
+  if (!e) return fail(WQ4_ENOMEM, "range tier 2: FFN workspace allocation failed");
+  for (DecGroup& g : m->groups) {
+    g.ffn_ws = m->dev.alloc<uint8_t>(nd);
+    if (!g.ffn_ws) return fail(WQ4_ENOMEM, "range tier 2: FFN workspace allocation failed");
+    g.ffn_ws_bytes = nd;
+    m->bytes += nd;
+  }
+  m->ffn_ws = e;
+  m->ffn_ws_bytes = ne;
+  m->bytes += ne;
+  return WQ4_OK;
 }
 
 // Number of decode groups for a batch (WA_DECODE_GROUPS overrides).
@@ -1526,6 +1516,16 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
                         &overflow);
     if (s != WQ4_OK) return s;
   }
+  if (overflow && !m->wide_ffn) {
+    // the FFN hidden layer (fc1 + GELU) feeds fc2 unnormalised: retry with
+    // every FFN on per-call operand scales (sticky, like tier 1)
+    s = ensure_ffn_ws(m);
+    if (s != WQ4_OK) return s;
+    m->wide_ffn = true;
+    s = transcribe_once(m, mel_dev, n_clips, lang_token, max_tokens, eot_stop, tokens_out, n_tokens_out, stream,
+                        &overflow);
+    if (s != WQ4_OK) return s;
+  }
   if (overflow)
     return fail(WQ4_ERANGE,
                 "activation overflow: an MFMA operand left the f16-pair range (|x| >= 4094 after the LayerNorm, "
@@ -1533,14 +1533,7 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
   return WQ4_OK;
 }
 
-int wa_model_wide_range(const wa_model* m) { return m ? (m->wide_range ? 1 : 0) : -1; }
-
-int wa_model_set_fused_projections(wa_model* m, int mask) {
-  if (!m || mask < -1 || mask > 7) return -1;
-  const int prev = m->fuse_proj;
-  m->fuse_proj = mask < 0 ? kFuseDefault : mask;
-  return prev;
-}
+int wa_model_wide_range(const wa_model* m) { return m ? (m->wide_ffn ? 2 : m->wide_range ? 1 : 0) : -1; }
 
 wq4_status wa_transcribe_trace(wa_model* m, const float* mel_dev, int n_clips, int lang_token, int max_tokens,
                                int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out, const int32_t* trace_ids_dev,

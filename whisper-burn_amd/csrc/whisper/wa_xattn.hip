@@ -28,7 +28,6 @@
 
 #include "../wq4_device.hpp"
 #include "../wq4_lnmath.hpp"
-#include "wa_headproj.hpp"
 #include "wa_kernels.hpp"
 
 namespace wa {
@@ -191,124 +190,6 @@ __global__ __launch_bounds__(128) void xattn_q_mfma_kernel(const float* __restri
       split_f16(acc[i] * kXqInv * kXqScale * kQtScale, x, y);
       qt[(((size_t)r * NS + 0) * HP + h) * D + c0 + c] = x;
       if (NS == 2) qt[(((size_t)r * NS + 1) * HP + h) * D + c0 + c] = y;
-    }
-  }
-}
-
-// The decode step's query (cq GEMM, cross_attn_ln folded) and qt = Wk^T q
-// in ONE launch for a group of <= 16 clips (Tq = 1, Q4_0 weights, f16x2):
-// workgroup = head h, 8 waves.  Stage 1 forms q_h for every row with the
-// decode-step GEMM's arithmetic (wa_headproj.hpp, ROWS = 16: Wq_h's 4 column
-// subtiles, the rows' A-tiled fold operand, tile statistics and fold vectors
-// by LDS-DMA; the same bits as the cq GEMM under kernel policy 3); stage 2 is
-// xattn_q_mfma_kernel's product for all D columns of the head (wave w:
-// 32-column tiles w, w + 8, ...; the same MFMA sequence per output, so the
-// same bits as that kernel on the same q).  The cq GEMM launch leaves the
-// chain, and the head's Wk block loads are in flight during stage 1.
-template <int NS>
-__global__ __launch_bounds__(512) void xattn_q_fused_kernel(HeadProj p, int R, int D, const uint8_t* __restrict__ wk,
-                                                            int HP, _Float16* __restrict__ qt) {
-  constexpr int LD = 72;
-  constexpr int TPW = kMaxD / 32 / 8;  // 32-column tiles per wave (<= 5)
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  __shared__ __attribute__((aligned(16))) float qs[16][64];
-  __shared__ float srow[16][2];
-  const int h = blockIdx.x, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  const int nkb = D / 32;
-  // stage 2's Wk blocks (row h * 64 + l, blocks w + 8 i) as raw u16 words:
-  // issued first, they land while stage 1 runs
-  uint16_t wraw[TPW][9];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int cb = w + 8 * i;
-    const uint16_t* blk = reinterpret_cast<const uint16_t*>(wk + ((size_t)(h * 64 + l) * nkb + (cb < nkb ? cb : 0)) * 18);
-#pragma unroll
-    for (int e = 0; e < 9; ++e) wraw[i][e] = blk[e];
-  }
-  hp_issue<16, 4>(p, [&](int s) { return 4 * h + s; }, 0, R, smem, w, 8, l);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (w < 4) {  // row 4 w + (l >> 4): its 16-lane group merges its tile statistics
-    float mean, den;
-    const int r = 4 * w + (l >> 4);
-    hp_row_stats<16, 4>(p, smem, r, l, mean, den);
-    if ((l & 15) == 0) {
-      srow[r][0] = mean;
-      srow[r][1] = den;
-    }
-  }
-  {
-    wq4::floatx4 acc[1][4];
-    hp_compute<16, 4, 1>(p, smem, w, 8, l, acc);
-    __syncthreads();  // every wave past its MFMAs: the partials overwrite W / D / A
-    hp_store_red<16, 4, 1>(p, smem, w, 8, l, acc);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {  // q_h of (row rr, column c)
-    const int o = tid + 512 * j, rr = o >> 6, c = o & 63;
-    qs[rr][c] = rr < R ? hp_finish<16, 4>(p, smem, rr, c, srow[rr][0], srow[rr][1]) : 0.0f;
-  }
-  __syncthreads();  // q complete; the partials are dead: stage 2 reuses the LDS
-  // stage 2 (xattn_q_mfma_kernel's product): A fragments, row l & 31, d = 16 ks + 8 kh ..
-  const int l32 = l & 31, kh = l >> 5;
-  half8 ah[4], al[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      _Float16 x, y;
-      wq4::split_act(l32 < 16 ? qs[l32][ks * 16 + 8 * kh + j] : 0.0f, x, y);
-      ah[ks][j] = x;
-      al[ks][j] = y;
-    }
-  _Float16* wth = reinterpret_cast<_Float16*>(smem) + (size_t)w * 2 * 32 * LD;
-  _Float16* wtl = wth + 32 * LD;
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int cb = w + 8 * i;
-    if (cb >= nkb) break;  // wave-uniform
-    {  // lane = weight row d of the head: its block cb, exact values, split, stored transposed
-      const float d = (float)__builtin_bit_cast(_Float16, wraw[i][0]);
-      float v[32];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {  // load_w32's element order
-        const uint32_t two = wraw[i][1 + e];
-        v[2 * e] = (float)((int)(two & 15u) - 8) * d;
-        v[2 * e + 1] = (float)((int)((two >> 8) & 15u) - 8) * d;
-        v[16 + 2 * e] = (float)((int)((two >> 4) & 15u) - 8) * d;
-        v[16 + 2 * e + 1] = (float)((int)((two >> 12) & 15u) - 8) * d;
-      }
-#pragma unroll
-      for (int e = 0; e < 32; ++e) {
-        _Float16 hi, lo;
-        split_f16(v[e] * kWkScale, hi, lo);
-        wth[e * LD + l] = hi;
-        wtl[e * LD + l] = lo;
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's transposed stores before its reads
-    __builtin_amdgcn_wave_barrier();
-    floatx16 acc = {};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const half8 bh = *reinterpret_cast<const half8*>(&wth[l32 * LD + ks * 16 + 8 * kh]);
-      const half8 bl = *reinterpret_cast<const half8*>(&wtl[l32 * LD + ks * 16 + 8 * kh]);
-      acc = mfma32x16(ah[ks], bh, acc);
-      acc = mfma32x16(al[ks], bh, acc);
-      acc = mfma32x16(ah[ks], bl, acc);
-    }
-    __builtin_amdgcn_wave_barrier();  // reads done before the next tile's stores
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int r = (e & 3) + 8 * (e >> 2) + 4 * kh;
-      if (r < R) {
-        _Float16 x, y;
-        split_f16(acc[e] * kXqInv * kXqScale * kQtScale, x, y);
-        qt[(((size_t)r * NS + 0) * HP + h) * D + cb * 32 + l32] = x;
-        if (NS == 2) qt[(((size_t)r * NS + 1) * HP + h) * D + cb * 32 + l32] = y;
-      }
     }
   }
 }
@@ -1202,31 +1083,18 @@ hipError_t launch_wv_pack(const uint8_t* wv, int H, int D, uint32_t* out, hipStr
   return hipGetLastError();
 }
 
-bool xattn_fused_q_supported(int R, int Tq, int D, int wtype, int ns) {
-  return Tq == 1 && R >= 1 && R <= 16 && wtype == kWtQ4 && ns == 2 && hp_supported(16, 4, D) &&
-         D / 32 <= 8 * (kMaxD / 32 / 8) && 8 * 2 * 32 * 72 * 2 <= hp_lds_bytes(16, 4, D / 128);
-}
-
 hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, const uint32_t* wvp, const float* bv,
                         int wtype, const _Float16* enc, int B, int Tq, int T, int H, int D, _Float16* qt, float* part,
-                        _Float16* tiled, int ns, hipStream_t st, const HeadProj* fuse) {
+                        _Float16* tiled, int ns, hipStream_t st) {
   const int R = B * Tq;
   const int HT = (H + 15) / 16, HP = HT * 16;
-  if (D != H * 64 || D % 128 != 0 || D > kMaxD || H > 20) return hipErrorInvalidValue;
+  if (D != H * 64 || D % 128 != 0 || D > kMaxD || H > 20 || !q) return hipErrorInvalidValue;
   if (wtype == kWtQ4 && !wvp) return hipErrorInvalidValue;  // Q4: the load-time packed Wv (launch_wv_pack)
   const XattnPlan p = xattn_plan(R, T);
   float* z = part;
   float* ml = part + (size_t)R * p.splits * H * D;
-  if (fuse && (!xattn_fused_q_supported(R, Tq, D, wtype, ns) || fuse->K != D || fuse->ku * 128 != D ||
-               !fuse->q16 || !fuse->d16 || !fuse->at || !fuse->stats || !fuse->wg || !fuse->b2))
-    return hipErrorInvalidValue;
-  if (!fuse && !q) return hipErrorInvalidValue;
-  // qt = Wk^T q / 8 (with the query itself formed in the launch when fused)
+  // qt = Wk^T q / 8
   const dim3 gq(H, D / 64, (R + 31) / 32);
-  if (fuse) {
-    hipLaunchKernelGGL(xattn_q_fused_kernel<2>, dim3(H), dim3(512), (size_t)hp_lds_bytes(16, 4, fuse->ku), st, *fuse,
-                       R, D, wk, HP, qt);
-  } else
 #define WA_XQ(NS_, WK_) hipLaunchKernelGGL((xattn_q_mfma_kernel<NS_, WK_>), gq, dim3(128), 0, st, q, R, D, wk, HP, qt)
   if (wtype == kWtQ4) {
     if (ns == 2) WA_XQ(2, kWtQ4); else WA_XQ(1, kWtQ4);

@@ -373,16 +373,6 @@ wq4_status wq4_tensor_create_f16(int device, const uint16_t* w, int64_t n, int64
 
 int wq4_tensor_has_decode_step(const wq4_tensor* t) { return t && t->q16 ? 1 : 0; }
 
-wq4_status wq4_tensor_decode_layout(const wq4_tensor* t, const uint32_t** q16, const uint16_t** d16, int64_t* ku) {
-  if (!t || !q16 || !d16 || !ku) return fail(WQ4_EINVAL, "null argument");
-  if (!t->q16 || !t->d16 || t->wtype != wq4::kWeightsQ4)
-    return fail(WQ4_EUNSUPPORTED, "tensor has no Q4_0 decode-step layout");
-  *q16 = t->q16;
-  *d16 = t->d16;
-  *ku = wq4::skinny_units(t->g);
-  return WQ4_OK;
-}
-
 // The decode-step kernel keeps f16 weights as w * 2^8 (wq4_skinny.hip): only
 // when that stays finite in f16 (|w| < 255.875).
 static bool f16_skinny_in_range(const uint16_t* w, size_t count) {

@@ -102,9 +102,8 @@ __host__ __device__ inline int kbp_of(int k) { return ((k / 32 + 1) / 2) * 2; }
 
 // The LayerNorm-fold consumer's correction (a - mean * (W gamma)[n]) / den
 // with the product-difference as ONE explicit fma: every kernel implementing
-// the consumer (the 8-wave decode kernel, the decode-step kernel, the
-// in-launch projections of wa_headproj.hpp) shares it, so floating-point
-// contraction cannot make their bits differ.
+// the consumer (the 8-wave decode kernel, the decode-step kernel) shares it,
+// so floating-point contraction cannot make their bits differ.
 __device__ __forceinline__ float lnf_apply(float a, float mean, float wg, float den) {
   return fmaf(-mean, wg, a) / den;
 }

@@ -55,8 +55,6 @@ def lib() -> ctypes.CDLL:
         L.wa_model_weight_type.restype = c_int
         L.wa_model_wide_range.argtypes = [vp]
         L.wa_model_wide_range.restype = c_int
-        L.wa_model_set_fused_projections.argtypes = [vp, c_int]
-        L.wa_model_set_fused_projections.restype = c_int
         L.wa_model_create_from_gguf.argtypes = [c_int, ctypes.c_char_p, c_int, c_int, c_int, ctypes.POINTER(vp)]
         L.wa_gguf_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
         L.wa_gguf_close.argtypes = [vp]
@@ -295,19 +293,14 @@ class WhisperModel:
     @property
     def wide_range(self) -> bool:
         """True once a transcribe overflowed the LayerNorm fold's operand range
-        and the model switched to the LayerNorm path (wa_model_wide_range)."""
-        return lib().wa_model_wide_range(self._h) == 1
+        and the model switched to the LayerNorm path (wa_model_wide_range >= 1)."""
+        return lib().wa_model_wide_range(self._h) >= 1
 
-    def set_fused_projections(self, mask: int) -> int:
-        """Diagnostics (wa_model_set_fused_projections): bit 0 the few-clip
-        self-attention's q / k / v, bit 1 the cross-attention query formed
-        inside the attention launches, bit 2 (with bit 0) the self-attention's
-        projection spread over 8 workgroups per head; -1 = the product default.  Returns the
-        previous mask."""
-        prev = lib().wa_model_set_fused_projections(self._h, int(mask))
-        if prev < 0:
-            raise ValueError(f"bad fused-projection mask {mask}")
-        return prev
+    @property
+    def range_tier(self) -> int:
+        """0 the product path, 1 the LayerNorm path, 2 the LayerNorm path with
+        every FFN on per-call operand scales (wa_model_wide_range)."""
+        return lib().wa_model_wide_range(self._h)
 
     def device_bytes(self) -> int:
         return int(lib().wa_model_device_bytes(self._h))
