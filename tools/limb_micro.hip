@@ -82,7 +82,7 @@ __device__ __forceinline__ intx4 deq_i8(u32x2 w) {
 }
 
 template <int F>
-__global__ __launch_bounds__(256) void block_loop(int nblk, float* sink) {
+__global__ __launch_bounds__(512) void block_loop(int nblk, float* sink) {
   __shared__ unsigned wq[1024];
   __shared__ _Float16 ds[512];
   const int tid = threadIdx.x, l = tid & 63;
@@ -168,6 +168,7 @@ double run(int wgs, int waves, int nblk, float* sink) {
   hipLaunchKernelGGL(block_loop<F>, dim3(wgs), dim3(64 * waves), 0, nullptr, 16, sink);
   CHECK(hipEventRecord(a, nullptr));
   hipLaunchKernelGGL(block_loop<F>, dim3(wgs), dim3(64 * waves), 0, nullptr, nblk, sink);
+  CHECK(hipGetLastError());  // a launch the resources refuse must not read as a fast kernel
   CHECK(hipEventRecord(b, nullptr));
   CHECK(hipEventSynchronize(b));
   float ms = 0;
