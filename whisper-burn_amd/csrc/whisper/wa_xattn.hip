@@ -73,6 +73,16 @@ constexpr int kXattnSplits = WA_XATTN_SPLITS;
 #ifndef WA_XATTN_DIAG
 #define WA_XATTN_DIAG 0
 #endif
+// WA_XATTN_STAMP (tools/xattn_micro.hip only): the clock at the phase
+// boundaries of every sub-chunk of workgroup (0, 0), waves 0 and NW - 1,
+// into g_xstamp (read back with hipMemcpyFromSymbol; results unchanged).
+#ifndef WA_XATTN_STAMP
+#define WA_XATTN_STAMP 0
+#endif
+#if WA_XATTN_STAMP
+constexpr int kXsPhases = 8, kXsChunks = 16;
+__device__ unsigned long long g_xstamp[2][kXsChunks][kXsPhases];
+#endif
 // xattn_out attribution builds (tools/xattn_micro.hip only, wrong results):
 // 1 = no Wv stage, 2 = no split-partial loads, 3 = no projection MFMAs.
 #ifndef WA_XATTN_ODIAG
@@ -227,7 +237,7 @@ __device__ __forceinline__ void softmax_entry(float sv, bool valid, float& M, fl
 // heads, k = the 16 frames read transposed from the same LDS image by
 // ds_read_b64_tr_b16; accumulators stay in registers).  Writes per (row,
 // split): Z [H][D] and (max, sum) [H].
-template <int D, int HT, int NS, int NW, int PF>
+template <int D, int HT, int NS, int NW, int PF, bool V2>
 __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __restrict__ qt,
                                                              const _Float16* __restrict__ enc, int Tq, int T,
                                                              int H, int S, int CH, float* __restrict__ zpart,
@@ -258,6 +268,16 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   const int ts = s * CH * kTc;
   const int te = min(T, ts + CH * kTc);
   const int nch = WA_XATTN_DIAG == 10 ? 0 : te > ts ? (te - ts + kTc - 1) / kTc : 0;
+#if WA_XATTN_STAMP
+  const int stamp_w = (s == 0 && r == 0 && l == 0) ? (w == 0 ? 0 : w == NW - 1 ? 1 : -1) : -1;
+  auto stamp = [&](int chi, int ph) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    const unsigned long long t = __builtin_readcyclecounter();
+    if (stamp_w >= 0 && chi < kXsChunks) g_xstamp[stamp_w][chi][ph] = t;
+  };
+#else
+  auto stamp = [](int, int) {};
+#endif
 
   // qt operands (B of the score MFMA: k = column, n = head): head tile 0 in
   // registers; for H in (16, 20] the 4 heads of tile 1 from LDS (registers of
@@ -336,7 +356,6 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   // store groups conflict-free.  Every wave touches only its own slice, so
   // the stores need no barrier before this wave's reads.
   auto sw = [](int t) { return (t & 8) ? 3 : 0; };
-  const int tcol_sw = ((((tcol >> 3) ^ sw(trow)) << 3) | (tcol & 7));  // rows trow and trow + 4 share sw
   const int lq_sw = lq ^ sw(l16);
   auto write_se = [&](const u32x4v (&buf)[NLD]) {
 #pragma unroll
@@ -379,9 +398,9 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
 #pragma unroll
     for (int ht = 0; ht < HT; ++ht) *reinterpret_cast<floatx4*>(&red[w][ht][l16][4 * lq]) = sacc[ht];
   };
-  // online softmax of the sub-chunk's scores (red) and the Z update from se
-  auto tail = [&](int chi, int t0) {
-    // online softmax: entry (head tile, head, frame); 16 lanes per head
+  // online softmax of the sub-chunk's scores (red): P to sp, alpha to salpha
+  auto softmax_phase = [&](int chi, int t0) {
+    // entry (head tile, head, frame); 16 lanes per head
 #pragma unroll
     for (int e = 0; e < SMX; ++e) {
       const int idx = tid + e * kThreads;
@@ -403,13 +422,15 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
         if (alpha != 1.0f && WA_XATTN_DIAG != 5) srescale[chi & 1] = 1;  // benign race: every writer stores 1
       }
     }
-    if (WA_XATTN_DIAG != 7) __syncthreads();
+  };
+  // the Z update of sub-chunk chi from se (rows at swizzle swz) and sp; call
+  // after the barrier that follows softmax_phase(chi)
+  auto z_phase = [&](int chi, auto&& swz, auto&& after_tile) {
     // alpha == 1 for every head (no running maximum moved, the steady state)
     // makes the rescale a multiplication by 1: skipped, bit-identical
     const bool rescale = srescale[chi & 1] != 0;
-    if (tid == 0) srescale[(chi + 1) & 1] = 0;  // next sub-chunk's flag; its writers come after the next score barrier
-
-    // Z update: A = P (m = head, k = frame), B = enc (k = frame, n = column)
+    if (tid == 0) srescale[(chi + 1) & 1] = 0;  // next sub-chunk's flag; its writers come after the next barrier
+    // A = P (m = head, k = frame), B = enc (k = frame, n = column)
     half8 pa[NS];
 #pragma unroll
     for (int p = 0; p < NS; ++p) pa[p] = *reinterpret_cast<const half8*>(&sp[p][l32][8 * lh]);
@@ -421,16 +442,19 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
         for (int ct = 0; ct < KS; ++ct) zacc[ct][j] *= al;
       }
     }
+    stamp(chi, 6);
+    const int tc0 = ((((tcol >> 3) ^ swz(trow)) << 3) | (tcol & 7));
+    const int tc1 = ((((tcol >> 3) ^ swz(trow + 4)) << 3) | (tcol & 7));
 #pragma unroll
     for (int ct = 0; ct < (WA_XATTN_DIAG == 2 ? 0 : KS); ++ct) {
       half8 eb[NS];
 #pragma unroll
       for (int p = 0; p < NS; ++p) {
-        const _Float16* base = &se[trow * RS + p * D + c0 + ct * 32 + tcol_sw];
-        const half4 x0 = lds_tr4(base);
-        const half4 x1 = lds_tr4(base + 4 * RS);
+        const half4 x0 = lds_tr4(&se[trow * RS + p * D + c0 + ct * 32 + tc0]);
+        const half4 x1 = lds_tr4(&se[(trow + 4) * RS + p * D + c0 + ct * 32 + tc1]);
         eb[p] = half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
       }
+      after_tile(ct);  // this tile's se reads are issued: the caller may overwrite it
       zacc[ct] = mfma32x16(pa[0], eb[0], zacc[ct]);
       if (NS == 2) {
         zacc[ct] = mfma32x16(pa[1], eb[0], zacc[ct]);
@@ -442,14 +466,92 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   // se, then one barrier for the score partials and one inside tail().
   auto step = [&](u32x4v (&buf)[NLD], int chi) {
     const int t0 = ts + chi * kTc;
+    stamp(chi, 0);
     write_se(buf);
+    stamp(chi, 1);
     if (chi + PF < nch && WA_XATTN_DIAG != 1) fetch(buf, chi + PF);  // in flight during the next PF sub-chunks
     scores([&](int ks, int p) {
       return *reinterpret_cast<const half8*>(&se[l16 * RS + p * D + c0 + ks * 32 + 8 * lq_sw]);
     });
+    stamp(chi, 2);
     if (WA_XATTN_DIAG != 6) __syncthreads();  // every wave's score partials in red
-    tail(chi, t0);
+    stamp(chi, 3);
+    softmax_phase(chi, t0);
+    stamp(chi, 4);
+    if (WA_XATTN_DIAG != 7) __syncthreads();
+    stamp(chi, 5);
+    z_phase(chi, sw, [](int) {});
+    stamp(chi, 7);
   };
+  if constexpr (V2) {
+    // V2: the scores read their A fragments straight from the fetched
+    // registers (lane (frame l16, k-group lq) loads exactly its fragments),
+    // so sub-chunk chi + 1's score MFMAs need no LDS image and run beside
+    // sub-chunk chi's Z update; the slice goes to se (for the transposed Z
+    // reads) tile by tile behind the Z reads of the same tile, and the fetch
+    // of sub-chunk chi + 2 follows each tile.  Per sub-chunk: scores(chi + 1)
+    // + Z(chi), barrier, softmax(chi + 1), barrier.  Same MFMAs in the same
+    // order on the same values as the staged form: the same bits.
+    // se swizzle sw2 (slot ^ (bit 1 of t ? 1 : 0) ^ (bit 2 of t ? 2 : 0),
+    // inside aligned 4-slot blocks): conflict-free for these fragment-order
+    // ds_write_b128 groups and for the transposed reads (rows t and t + 4
+    // differ: each half of a fragment uses its own row's swizzle).
+    auto sw2 = [](int t) { return ((t & 2) ? 1 : 0) ^ ((t & 4) ? 2 : 0); };
+    u32x4v fb[KS][NS];
+    auto fetch2 = [&](int chi, int ks) {
+#pragma unroll
+      for (int p = 0; p < NS; ++p)
+        fb[ks][p] = __builtin_amdgcn_raw_buffer_load_b128(
+            rs, (uint32_t)(((chi * kTc + l16) * ROW + p * D + c0 + ks * 32 + 8 * lq) * 2), 0, 0);
+    };
+    auto write_tile = [&](int ks) {
+#pragma unroll
+      for (int p = 0; p < NS; ++p) {
+        const int col = p * D + c0 + ks * 32 + 8 * lq;
+        *reinterpret_cast<u32x4v*>(&se[l16 * RS + (((col >> 3) ^ sw2(l16)) << 3)]) = fb[ks][p];
+      }
+    };
+    auto scores2 = [&]() {
+      scores([&](int ks, int p) { return __builtin_bit_cast(half8, fb[ks][p]); });
+    };
+    if (nch > 0) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) fetch2(0, ks);
+    }
+    __syncthreads();  // sq1, sp, salpha, srescale, szero initialised
+    if (nch > 0) {
+      scores2();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        write_tile(ks);
+        if (nch > 1 && WA_XATTN_DIAG != 1) fetch2(1, ks);
+      }
+      __syncthreads();  // every wave's score partials of sub-chunk 0 in red
+      softmax_phase(0, ts);
+      __syncthreads();
+    }
+    for (int chi = 0; chi < nch; ++chi) {
+      const bool more = chi + 1 < nch;
+      stamp(chi, 0);
+      if (more) scores2();  // sub-chunk chi + 1 (red is free: softmax(chi) read it before the last barrier)
+      stamp(chi, 2);
+      z_phase(chi, sw2, [&](int ct) {
+        if (more) {
+          write_tile(ct);  // sub-chunk chi + 1 into this tile of the slice (its chi reads are issued)
+          if (chi + 2 < nch && WA_XATTN_DIAG != 1) fetch2(chi + 2, ct);
+        }
+      });
+      stamp(chi, 3);
+      if (more) {
+        __syncthreads();  // red (scores chi + 1) complete; every wave's Z(chi) reads of sp / salpha done
+        stamp(chi, 4);
+        softmax_phase(chi + 1, ts + (chi + 1) * kTc);
+        stamp(chi, 5);
+        __syncthreads();  // sp / salpha / srescale of chi + 1
+      }
+      stamp(chi, 7);
+    }
+  } else {
   u32x4v pre0[NLD];
   u32x4v pre1[PF == 2 ? NLD : 1];
   if (nch > 0) fetch(pre0, 0);
@@ -462,6 +564,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     }
   } else {
     for (int chi = 0; chi < nch; ++chi) step(pre0, chi);
+  }
   }
 
   // partials of this (row, split)
@@ -571,15 +674,19 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
   }
   // merge of the S frame ranges (flash-attention merge, fixed split order):
   // Zn[c] = (sum_s w_s Z_s[c]) / (sum_s w_s L_s), w_s = exp(M_s - max_s M_s).
-  // Item (row j, 4 columns): the row's (M_s, L_s) and every split's float4.
-  // All NIT items of a thread are loaded before any is merged (fixed
-  // unrolled counts; splits >= S read nothing), so the merge costs one memory
-  // round trip; rows >= R give zeros.
+  // The weights depend on the row only: thread (row j < RPW) computes its
+  // row's w_s and the denominator (split order) into LDS while every
+  // thread's Z loads are in flight -- one memory round trip for the merge and
+  // no per-item copies of (M_s, L_s) in registers (at 12-16 splits those
+  // spilled: xattn_out 16-36 us, profiles/r05_xattn_micro.log).  Item (row j,
+  // 4 columns): every split's float4, all NIT items loaded before any is
+  // merged (fixed unrolled counts; splits >= S read nothing); rows >= R give
+  // zeros.
+  __shared__ float swt[RPW][SM + 1];  // w_s per row, [SM] = the denominator
   {
     const int nq = D / 4;
     constexpr int NIT = (RPW * (kMaxD / 4) + 511) / 512;
     floatx4 zv[NIT][SM];
-    floatx2 ml[NIT][SM];
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
       const int it = tid + 512 * u;
@@ -587,34 +694,48 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
       const bool ok = it < RPW * nq && rbase + rstep * j < R;
       const size_t rb = (size_t)(ok ? rbase + rstep * j : 0) * S;
       const floatx4* zp = reinterpret_cast<const floatx4*>(zpart + (rb * H + h) * D) + (ok ? q : 0);
+#pragma unroll
+      for (int s = 0; s < SM; ++s)
+        if (s < S) zv[u][s] = WA_XATTN_ODIAG == 2 ? floatx4{0.0f, 0.0f, 0.0f, 0.0f} : zp[(size_t)s * H * (D / 4)];
+    }
+    if (tid < RPW) {
+      const int j = tid;
+      const size_t rb = (size_t)(rbase + rstep * j < R ? rbase + rstep * j : 0) * S;
       const floatx2* mp = reinterpret_cast<const floatx2*>(mlpart) + rb * H + h;
+      floatx2 ml[SM];
+#pragma unroll
+      for (int s = 0; s < SM; ++s)
+        if (s < S) ml[s] = WA_XATTN_ODIAG == 2 ? floatx2{0.0f, 1.0f} : mp[(size_t)s * H];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int s = 0; s < SM; ++s)
+        if (s < S) mx = fmaxf(mx, ml[s][0]);
+      float lsum = 0.0f;
 #pragma unroll
       for (int s = 0; s < SM; ++s)
         if (s < S) {
-          ml[u][s] = WA_XATTN_ODIAG == 2 ? floatx2{0.0f, 1.0f} : mp[(size_t)s * H];
-          zv[u][s] = WA_XATTN_ODIAG == 2 ? floatx4{0.0f, 0.0f, 0.0f, 0.0f} : zp[(size_t)s * H * (D / 4)];
+          const float w = ml[s][0] == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(ml[s][0] - mx);  // base-2 units
+          lsum = fmaf(w, ml[s][1], lsum);
+          swt[j][s] = w;
         }
+      swt[j][SM] = lsum;
     }
+    __syncthreads();
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
       const int it = tid + 512 * u;
       if (it >= RPW * nq) break;
       const int j = it / nq, q = it - j * nq;
       const bool rok = rbase + rstep * j < R;
-      float mx = -INFINITY;
-#pragma unroll
-      for (int s = 0; s < SM; ++s)
-        if (s < S) mx = fmaxf(mx, ml[u][s][0]);
-      float lsum = 0.0f;
       floatx4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int s = 0; s < SM; ++s)
         if (s < S) {
-          const float w = ml[u][s][0] == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(ml[u][s][0] - mx);  // base-2 units
-          lsum = fmaf(w, ml[u][s][1], lsum);
+          const float w = swt[j][s];
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc[e] = fmaf(w, zv[u][s][e], acc[e]);
         }
+      const float lsum = swt[j][SM];
       if constexpr (WK == kWtQ4) {
         half4 hi, lo;
 #pragma unroll
@@ -983,13 +1104,27 @@ int xattn_small_rows() {
 // eighth of the columns + one sub-chunk in flight); 4 when D / 8 is not a
 // multiple of 32 (D = 384).  A second sub-chunk in flight (PF = 2) does not
 // fit the register file at Large-V3 f16x2.
+// The sub-chunk loop: 0 = staged (write the slice to se, scores from se), 1
+// = V2 (scores from the fetched registers beside the previous sub-chunk's Z
+// update); WA_XATTN_MAIN overrides (read per launch, like
+// WA_XATTN_SMALL_ROWS: tests switch it).  Both give the same bits.
+int xattn_main_form() {
+  const char* e = getenv("WA_XATTN_MAIN");
+  return e ? atoi(e) : 0;
+}
 template <int D, int HT, int NS>
 void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T, int H, int S, int CH, float* z,
-                 float* ml, int R, hipStream_t st) {
-  if constexpr ((D / 8) % 32 == 0)
-    hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 8, 1>), g, dim3(512), 0, st, qt, enc, Tq, T, H, S, CH, z, ml, R);
-  else
-    hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, 4, 1>), g, dim3(256), 0, st, qt, enc, Tq, T, H, S, CH, z, ml, R);
+                 float* ml, int R, hipStream_t st, int form = -1) {
+  const bool v2 = (form < 0 ? xattn_main_form() : form) == 1;
+#define WA_XM(NW_, V2_) \
+  hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, NW_, 1, V2_>), g, dim3(64 * NW_), 0, st, qt, enc, Tq, T, H, S, CH, \
+                     z, ml, R)
+  if constexpr ((D / 8) % 32 == 0) {
+    if (v2) { WA_XM(8, true); } else { WA_XM(8, false); }
+  } else {
+    if (v2) { WA_XM(4, true); } else { WA_XM(4, false); }
+  }
+#undef WA_XM
 }
 
 // Rows of Zn per xattn_out workgroup: 4.  Isolated, 2 rows per workgroup is

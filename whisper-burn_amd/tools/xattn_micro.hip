@@ -85,8 +85,12 @@ int main(int argc, char** argv) {
       return ms * 1e3f / iters;
     };
     const float t_main = time_it([&] {
-      wa::launch_main<1280, 2, 2>(dim3(p.splits, R), qt, enc, 1, T, H, p.splits, p.ch, z, ml, R, 0);
+      wa::launch_main<1280, 2, 2>(dim3(p.splits, R), qt, enc, 1, T, H, p.splits, p.ch, z, ml, R, 0, 0);
     });
+    const float t_main2 = time_it([&] {
+      wa::launch_main<1280, 2, 2>(dim3(p.splits, R), qt, enc, 1, T, H, p.splits, p.ch, z, ml, R, 0, 1);
+    });
+    printf("{\"rows\": %d, \"main_staged_us\": %.2f, \"main_v2_us\": %.2f}\n", R, t_main, t_main2);
     const float t_q = time_it([&] {
       hipLaunchKernelGGL((wa::xattn_q_mfma_kernel<2, wa::kWtQ4>), dim3(H, D / 64, (R + 31) / 32), dim3(128), 0, 0,
                          q, R, D, wk, HP, qt);
@@ -114,6 +118,29 @@ int main(int argc, char** argv) {
       });
     }
     CK(hipGetLastError());
+#if WA_XATTN_STAMP
+    {  // phase durations of workgroup (0, 0) in the last timed main launch (clock cycles)
+      (void)time_it([&] {
+        wa::launch_main<1280, 2, 2>(dim3(p.splits, R), qt, enc, 1, T, H, p.splits, p.ch, z, ml, R, 0);
+      });
+      unsigned long long st[2][wa::kXsChunks][wa::kXsPhases];
+      CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(wa::g_xstamp), sizeof(st)));
+      static const char* names[] = {"write_se", "scores", "barrier1", "softmax", "barrier2", "rescale", "z"};
+      for (int wv = 0; wv < 2; ++wv) {
+        double tot[7] = {0, 0, 0, 0, 0, 0, 0};
+        double span = 0;
+        const int nch = p.ch;
+        for (int c = 0; c < nch && c < wa::kXsChunks; ++c) {
+          for (int ph = 0; ph < 7; ++ph) tot[ph] += (double)(st[wv][c][ph + 1] - st[wv][c][ph]);
+          span += (double)(st[wv][c][7] - st[wv][c][0]);
+        }
+        printf("{\"rows\": %d, \"wave\": \"%s\", \"chunks\": %d, \"cycles_per_chunk\": %.0f", R, wv ? "last" : "first",
+               nch, span / nch);
+        for (int ph = 0; ph < 7; ++ph) printf(", \"%s\": %.0f", names[ph], tot[ph] / nch);
+        printf("}\n");
+      }
+    }
+#endif
     printf("{\"rows\": %d, \"scores_us\": %.2f, \"z_us\": %.2f}\n", R, t_sc, t_z);
     const double bytes = (double)R * T * D * 2 * NS;
     printf("{\"small\": %d, \"diag\": %d, \"rows\": %d, \"splits\": %d, \"main_us\": %.2f, \"q_us\": %.2f, \"out_us\": %.2f, "
