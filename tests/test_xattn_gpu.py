@@ -114,32 +114,6 @@ def test_xattn_small_rows_bit_identical(torch, monkeypatch, B, Tq, T, H):
     assert np.abs(split - ref).max() / np.abs(ref).max() <= 2e-5
 
 
-@pytest.mark.parametrize("B,Tq,T,H,prec", [
-    (16, 1, 1500, 20, wq4.PREC_F16X2),  # the bench's decode group (Large-V3, 16 clips)
-    (32, 1, 1500, 20, wq4.PREC_F16X2),  # one 32-clip group
-    (1, 1, 1500, 20, wq4.PREC_F16X2),   # one clip on the fused kernel
-    (2, 4, 1500, 20, wq4.PREC_F16X2),   # prompt rows
-    (6, 1, 1500, 16, wq4.PREC_F16X2),   # Medium (one head tile)
-    (5, 1, 200, 6, wq4.PREC_F16X2),     # test configuration (4 waves per slice)
-    (3, 1, 37, 20, wq4.PREC_F16X2),     # ragged last sub-chunk, one sub-chunk per split
-    (9, 1, 70, 20, wq4.PREC_F16X2),     # two sub-chunks per split, the second ragged
-    (16, 1, 1500, 20, wq4.PREC_F16),    # hi planes only
-])
-def test_xattn_main_forms_bit_identical(torch, monkeypatch, B, Tq, T, H, prec):
-    """The two sub-chunk loops of xattn_main_kernel (staged: scores from the
-    LDS image; V2: scores from the fetched registers beside the previous
-    sub-chunk's Z update, wa_xattn.hip) run the same MFMAs in the same order
-    on the same values: bit-identical outputs, within the reference bound."""
-    monkeypatch.setenv("WA_XATTN_SMALL_ROWS", "0")
-    monkeypatch.setenv("WA_XATTN_MAIN", "0")
-    staged, ref = run_case(torch, B, Tq, T, H, prec=prec, seed=21)
-    monkeypatch.setenv("WA_XATTN_MAIN", "1")
-    v2, _ = run_case(torch, B, Tq, T, H, prec=prec, seed=21)
-    assert np.array_equal(staged, v2), np.abs(staged - v2).max()
-    bound = 2e-5 if prec == wq4.PREC_F16X2 else 5e-3
-    assert np.abs(v2 - ref).max() / np.abs(ref).max() <= bound
-
-
 def test_xattn_small_rows_f16_precision(torch, monkeypatch):
     monkeypatch.setenv("WA_XATTN_SMALL_ROWS", "0")
     fused, _ = run_case(torch, 2, 1, 1500, 20, prec=wq4.PREC_F16, seed=12)

@@ -62,6 +62,8 @@ constexpr float kZnScale = 32.0f, kWvScale = 4096.0f, kOutInv = 1.0f / (32.0f * 
 // in round 2's model (two concurrent decode groups of 16 clips) 12 and 16 ran
 // the isolated 16-clip launch faster (50.5 us vs 55.7 at 12) but the decode
 // slower (926 / 1073 ms vs 873): more workgroups crowd out the other group.
+// Round 5 (after the xattn_out merge rewrite): 12 splits 30.1 vs 36.2 us
+// isolated at 16 rows, decode 909 vs 856 ms.
 constexpr int kXattnSplits = WA_XATTN_SPLITS;
 // Timing attribution builds of tools/xattn_micro.hip only (wrong results):
 // 1 = no encoder fetch after the first sub-chunk, 2 = no Z phase, 3 = no
@@ -237,7 +239,7 @@ __device__ __forceinline__ void softmax_entry(float sv, bool valid, float& M, fl
 // heads, k = the 16 frames read transposed from the same LDS image by
 // ds_read_b64_tr_b16; accumulators stay in registers).  Writes per (row,
 // split): Z [H][D] and (max, sum) [H].
-template <int D, int HT, int NS, int NW, int PF, bool V2>
+template <int D, int HT, int NS, int NW, int PF>
 __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __restrict__ qt,
                                                              const _Float16* __restrict__ enc, int Tq, int T,
                                                              int H, int S, int CH, float* __restrict__ zpart,
@@ -425,7 +427,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   };
   // the Z update of sub-chunk chi from se (rows at swizzle swz) and sp; call
   // after the barrier that follows softmax_phase(chi)
-  auto z_phase = [&](int chi, auto&& swz, auto&& after_tile) {
+  auto z_phase = [&](int chi) {
     // alpha == 1 for every head (no running maximum moved, the steady state)
     // makes the rescale a multiplication by 1: skipped, bit-identical
     const bool rescale = srescale[chi & 1] != 0;
@@ -443,8 +445,8 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
       }
     }
     stamp(chi, 6);
-    const int tc0 = ((((tcol >> 3) ^ swz(trow)) << 3) | (tcol & 7));
-    const int tc1 = ((((tcol >> 3) ^ swz(trow + 4)) << 3) | (tcol & 7));
+    const int tc0 = ((((tcol >> 3) ^ sw(trow)) << 3) | (tcol & 7));
+    const int tc1 = ((((tcol >> 3) ^ sw(trow + 4)) << 3) | (tcol & 7));
 #pragma unroll
     for (int ct = 0; ct < (WA_XATTN_DIAG == 2 ? 0 : KS); ++ct) {
       half8 eb[NS];
@@ -454,7 +456,6 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
         const half4 x1 = lds_tr4(&se[(trow + 4) * RS + p * D + c0 + ct * 32 + tc1]);
         eb[p] = half8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
       }
-      after_tile(ct);  // this tile's se reads are issued: the caller may overwrite it
       zacc[ct] = mfma32x16(pa[0], eb[0], zacc[ct]);
       if (NS == 2) {
         zacc[ct] = mfma32x16(pa[1], eb[0], zacc[ct]);
@@ -480,78 +481,9 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     stamp(chi, 4);
     if (WA_XATTN_DIAG != 7) __syncthreads();
     stamp(chi, 5);
-    z_phase(chi, sw, [](int) {});
+    z_phase(chi);
     stamp(chi, 7);
   };
-  if constexpr (V2) {
-    // V2: the scores read their A fragments straight from the fetched
-    // registers (lane (frame l16, k-group lq) loads exactly its fragments),
-    // so sub-chunk chi + 1's score MFMAs need no LDS image and run beside
-    // sub-chunk chi's Z update; the slice goes to se (for the transposed Z
-    // reads) tile by tile behind the Z reads of the same tile, and the fetch
-    // of sub-chunk chi + 2 follows each tile.  Per sub-chunk: scores(chi + 1)
-    // + Z(chi), barrier, softmax(chi + 1), barrier.  Same MFMAs in the same
-    // order on the same values as the staged form: the same bits.
-    // se swizzle sw2 (slot ^ (bit 1 of t ? 1 : 0) ^ (bit 2 of t ? 2 : 0),
-    // inside aligned 4-slot blocks): conflict-free for these fragment-order
-    // ds_write_b128 groups and for the transposed reads (rows t and t + 4
-    // differ: each half of a fragment uses its own row's swizzle).
-    auto sw2 = [](int t) { return ((t & 2) ? 1 : 0) ^ ((t & 4) ? 2 : 0); };
-    u32x4v fb[KS][NS];
-    auto fetch2 = [&](int chi, int ks) {
-#pragma unroll
-      for (int p = 0; p < NS; ++p)
-        fb[ks][p] = __builtin_amdgcn_raw_buffer_load_b128(
-            rs, (uint32_t)(((chi * kTc + l16) * ROW + p * D + c0 + ks * 32 + 8 * lq) * 2), 0, 0);
-    };
-    auto write_tile = [&](int ks) {
-#pragma unroll
-      for (int p = 0; p < NS; ++p) {
-        const int col = p * D + c0 + ks * 32 + 8 * lq;
-        *reinterpret_cast<u32x4v*>(&se[l16 * RS + (((col >> 3) ^ sw2(l16)) << 3)]) = fb[ks][p];
-      }
-    };
-    auto scores2 = [&]() {
-      scores([&](int ks, int p) { return __builtin_bit_cast(half8, fb[ks][p]); });
-    };
-    if (nch > 0) {
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) fetch2(0, ks);
-    }
-    __syncthreads();  // sq1, sp, salpha, srescale, szero initialised
-    if (nch > 0) {
-      scores2();
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        write_tile(ks);
-        if (nch > 1 && WA_XATTN_DIAG != 1) fetch2(1, ks);
-      }
-      __syncthreads();  // every wave's score partials of sub-chunk 0 in red
-      softmax_phase(0, ts);
-      __syncthreads();
-    }
-    for (int chi = 0; chi < nch; ++chi) {
-      const bool more = chi + 1 < nch;
-      stamp(chi, 0);
-      if (more) scores2();  // sub-chunk chi + 1 (red is free: softmax(chi) read it before the last barrier)
-      stamp(chi, 2);
-      z_phase(chi, sw2, [&](int ct) {
-        if (more) {
-          write_tile(ct);  // sub-chunk chi + 1 into this tile of the slice (its chi reads are issued)
-          if (chi + 2 < nch && WA_XATTN_DIAG != 1) fetch2(chi + 2, ct);
-        }
-      });
-      stamp(chi, 3);
-      if (more) {
-        __syncthreads();  // red (scores chi + 1) complete; every wave's Z(chi) reads of sp / salpha done
-        stamp(chi, 4);
-        softmax_phase(chi + 1, ts + (chi + 1) * kTc);
-        stamp(chi, 5);
-        __syncthreads();  // sp / salpha / srescale of chi + 1
-      }
-      stamp(chi, 7);
-    }
-  } else {
   u32x4v pre0[NLD];
   u32x4v pre1[PF == 2 ? NLD : 1];
   if (nch > 0) fetch(pre0, 0);
@@ -564,7 +496,6 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     }
   } else {
     for (int chi = 0; chi < nch; ++chi) step(pre0, chi);
-  }
   }
 
   // partials of this (row, split)
@@ -1103,28 +1034,16 @@ int xattn_small_rows() {
 // 8 waves (two per SIMD, 256 registers each: the Z accumulators of an
 // eighth of the columns + one sub-chunk in flight); 4 when D / 8 is not a
 // multiple of 32 (D = 384).  A second sub-chunk in flight (PF = 2) does not
-// fit the register file at Large-V3 f16x2.
-// The sub-chunk loop: 0 = staged (write the slice to se, scores from se), 1
-// = V2 (scores from the fetched registers beside the previous sub-chunk's Z
-// update); WA_XATTN_MAIN overrides (read per launch, like
-// WA_XATTN_SMALL_ROWS: tests switch it).  Both give the same bits.
-int xattn_main_form() {
-  const char* e = getenv("WA_XATTN_MAIN");
-  return e ? atoi(e) : 0;
-}
+// fit the register file at Large-V3 f16x2.  Measured and removed (round 5):
+// the scores of sub-chunk j + 1 straight from the fetched registers beside
+// sub-chunk j's Z update (one LDS write less, the MFMAs of two sub-chunks
+// interleaved) -- 45.3 vs 36.2 us at 16 rows, decode 970 vs 856 ms.
 template <int D, int HT, int NS>
 void launch_main(dim3 g, const _Float16* qt, const _Float16* enc, int Tq, int T, int H, int S, int CH, float* z,
-                 float* ml, int R, hipStream_t st, int form = -1) {
-  const bool v2 = (form < 0 ? xattn_main_form() : form) == 1;
-#define WA_XM(NW_, V2_) \
-  hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, NW_, 1, V2_>), g, dim3(64 * NW_), 0, st, qt, enc, Tq, T, H, S, CH, \
-                     z, ml, R)
-  if constexpr ((D / 8) % 32 == 0) {
-    if (v2) { WA_XM(8, true); } else { WA_XM(8, false); }
-  } else {
-    if (v2) { WA_XM(4, true); } else { WA_XM(4, false); }
-  }
-#undef WA_XM
+                 float* ml, int R, hipStream_t st) {
+  constexpr int NW = (D / 8) % 32 == 0 ? 8 : 4;
+  hipLaunchKernelGGL((xattn_main_kernel<D, HT, NS, NW, 1>), g, dim3(64 * NW), 0, st, qt, enc, Tq, T, H, S, CH, z, ml,
+                     R);
 }
 
 // Rows of Zn per xattn_out workgroup: 4.  Isolated, 2 rows per workgroup is

@@ -85,12 +85,8 @@ int main(int argc, char** argv) {
       return ms * 1e3f / iters;
     };
     const float t_main = time_it([&] {
-      wa::launch_main<1280, 2, 2>(dim3(p.splits, R), qt, enc, 1, T, H, p.splits, p.ch, z, ml, R, 0, 0);
+      wa::launch_main<1280, 2, 2>(dim3(p.splits, R), qt, enc, 1, T, H, p.splits, p.ch, z, ml, R, 0);
     });
-    const float t_main2 = time_it([&] {
-      wa::launch_main<1280, 2, 2>(dim3(p.splits, R), qt, enc, 1, T, H, p.splits, p.ch, z, ml, R, 0, 1);
-    });
-    printf("{\"rows\": %d, \"main_staged_us\": %.2f, \"main_v2_us\": %.2f}\n", R, t_main, t_main2);
     const float t_q = time_it([&] {
       hipLaunchKernelGGL((wa::xattn_q_mfma_kernel<2, wa::kWtQ4>), dim3(H, D / 64, (R + 31) / 32), dim3(128), 0, 0,
                          q, R, D, wk, HP, qt);
