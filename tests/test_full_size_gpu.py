@@ -260,3 +260,34 @@ def test_full_size_tokens_at_bench_shape(name):
             assert err <= tol, f"{name} (batch {B}): clip {b} step {s + 1}: |gpu - f64| {err:.3e} > {tol:.3e}"
     print(f"{name} in a batch of {B}: tokens equal ({n} x {steps}), worst logit error {worst:.3f} of the bound")
     m.close()
+
+
+@pytest.mark.gpu
+def test_full_size_tokens_pipelined():
+    """The bench's pipelined path (wa_transcribe_batches, the default bench
+    mode) at its shape: two batches of 32 Large-V3 Q4_0 clips holding the
+    fixture's clips at different positions, batch 1's encoder partly on the
+    CU-masked stream beside batch 0's decode; the fixture clips' 224 tokens
+    equal the f32 oracle's in both batches."""
+    import torch
+
+    import whisper_amd
+    from whisper_oracle import synthetic_mel
+
+    f, meta = _fixture("large_v3_q4")
+    clips, steps, lang = list(meta["clips"]), meta["steps"], meta["lang"]
+    B = 32
+    m = whisper_amd.WhisperModel(meta["variant"], meta["seed"], max_batch=B, weights=meta["weights"])
+    n_mels = m.config["n_mels"]
+    others = [2000 + c for c in range(B - len(clips))]
+    order = [clips + others, others[:5] + clips + others[5:]]
+    mel = torch.from_numpy(np.stack([np.stack([synthetic_mel(c, n_mels) for c in o]) for o in order])).cuda()
+    out = m.transcribe_batches(mel, lang, steps, eot_stop=False)
+    ref = f["tokens_f32"]
+    for i, o in enumerate(order):
+        for j, c in enumerate(clips):
+            b = o.index(c)
+            assert out[i][b] == [int(t) for t in ref[j, :steps]], f"batch {i} clip {c} (position {b})"
+    st = m.pipeline_stats()
+    print(f"pipelined bench shape: tokens equal in both batches; overlap {st}")
+    m.close()

@@ -59,6 +59,13 @@ wq4_status fail(wq4_status s, const std::string& m) {
 constexpr int kSOT = 50258;
 constexpr int kMaxTokens = 224;  // whisper.rs:20
 constexpr int kMinTokens = 3;    // whisper.rs:97
+// Pipelined transcribes (transcribe_pipelined): CUs of the encoder stream
+// that runs beside a decode, the encoder layers it covers in the first
+// overlapped batch, and the share of the last decode's length its part is
+// sized to afterwards (WA_ENC_CUS / WA_ENC_OVERLAP override).
+constexpr int kEncOverlapCUs = 32;
+constexpr int kEncOverlapLayers0 = 16;
+constexpr double kEncOverlapFill = 0.92;
 
 struct Config {  // WhisperConfig, src/model/config.rs:5-30
   int n_mels, n_audio_ctx, n_audio_state, n_audio_head, n_audio_layer;
@@ -245,6 +252,13 @@ struct wa_model {
   bool kv_alloc_ok = false;  // every layer's xk / xv allocated (cross_kv_forward)
   bool group_kv(const DecGroup& g) const { return g.nb > 0 && g.b0 + g.nb <= kv_n; }
   hipStream_t own_stream = nullptr;  // encoder / encoder planes (graph capture needs a non-null stream)
+  // pipelined transcribes (wa_transcribe_batches): the CU-masked stream of
+  // the encoder part that runs beside a decode, its CU count, the encoder
+  // layers that part covers (adapted per batch) and the last call's stats
+  hipStream_t enc_stream = nullptr;
+  int enc_cus = 0;
+  int overlap_k = -1;
+  float pipe[4] = {0, 0, 0, 0};
   // Activation-range guard.  Every internal producer writes MFMA operands as
   // f16 pairs of x * 2^4 (wq4_device.hpp split_act), finite for |x| < 4094;
   // beyond that the f16 half overflows and the clip's logits become inf /
@@ -303,6 +317,7 @@ struct wa_model {
       if (g.host_ndone) (void)hipHostFree(g.host_ndone);
     }
     if (own_stream) (void)hipStreamDestroy(own_stream);
+    if (enc_stream) (void)hipStreamDestroy(enc_stream);
     for (auto& l : enc)
       for (wq4_tensor* t : {l.qkv, l.out, l.fc1, l.fc2}) wq4_tensor_destroy(t);
     for (auto& l : dec)
@@ -726,7 +741,20 @@ wq4_status alloc_activations(wa_model* m) {
     WA_HIP(hipMemset(g.atd_dec, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
     WA_HIP(hipMemset(g.atf_dec, 0, wq4_atiled_bytes(rdec, Ft, m->prec)));
     WA_HIP(hipHostMalloc(reinterpret_cast<void**>(&g.host_ndone), 8 * sizeof(int), 0));
-    WA_HIP(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
+    if (const char* e = getenv("WA_DECODE_CUMASK"); e && atoi(e) > 0) {  // A/B: decode off the encoder's first n CUs
+      hipDeviceProp_t prop;
+      WA_HIP(hipGetDeviceProperties(&prop, m->device));
+      const int total = prop.multiProcessorCount;
+      std::vector<uint32_t> mask((total + 31) / 32, 0u);
+      for (int i = atoi(e); i < total; ++i) mask[i / 32] |= 1u << (i % 32);
+      WA_HIP(hipExtStreamCreateWithCUMask(&g.st, (uint32_t)mask.size(), mask.data()));
+    } else if (const char* e = getenv("WA_GROUP_PRIO"); e && atoi(e) != 0) {  // A/B probe (scripts/encode_overlap_probe.py)
+      int lo = 0, hi = 0;
+      WA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      WA_HIP(hipStreamCreateWithPriority(&g.st, hipStreamNonBlocking, atoi(e) > 0 ? hi : lo));
+    } else {
+      WA_HIP(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
+    }
   }
   m->range_flag = d.alloc<int>(1);
   for (void* p : {(void*)m->h1, (void*)m->x, (void*)m->qkv, (void*)m->at_d, (void*)m->at_f, (void*)m->enc_planes,
@@ -751,7 +779,9 @@ struct Prof {
   hipEvent_t a = nullptr, b = nullptr;
   Prof(wa_model* m_, hipStream_t st_, int cat_, double gflop_, double gb_)
       : m(m_), st(st_), cat(cat_), gflop(gflop_), gb(gb_) {
-    if (m->profile && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
+    // the CU-masked stream of a pipelined transcribe is not timed: the
+    // events measure the kernels at full width
+    if (m->profile && st != m->enc_stream && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
       (void)hipEventRecord(a, st);
   }
   ~Prof() {
@@ -770,14 +800,17 @@ Prof q4prof(wa_model* m, hipStream_t st, const wq4_tensor* w, int64_t rows) {
   return Prof(m, st, 0, 2.0 * rows * n * k * 1e-9, ((double)n * k * 18 / 32 + 4.0 * rows * k + 4.0 * rows * n) * 1e-9);
 }
 
-// WhisperEncoder::forward (encoder.rs:87-115) + ln_post (f32, into
-// enc_out_f32 or the conv scratch; m->enc_f32 points at it).
-wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st, float* enc_out_f32) {
+// WhisperEncoder::forward (encoder.rs:87-115) in three parts, so that a
+// pipelined transcribe (wa_transcribe_batches) can run the front and the
+// first layers of the next batch's encoder on a CU-masked stream beside the
+// current batch's decode: encoder_front (the conv stem), encoder_layers
+// [l0, l1) and encoder_post (ln_post, f32, into enc_out_f32 or the conv
+// scratch; m->enc_f32 points at it).
+wq4_status encoder_front(wa_model* m, const float* mel, int B, hipStream_t st) {
   const Config& c = m->cfg;
-  const int D = c.n_audio_state, T = c.n_audio_ctx, H = c.n_audio_head;
+  const int D = c.n_audio_state, T = c.n_audio_ctx;
   const int T_mel = 2 * T;
   const int64_t rows = (int64_t)B * T;
-  const double ln_gb = 8.0 * rows * D * 1e-9;
   {  // conv1 + GELU: mel [B, n_mels, 3000] -> h1 [B, 3000, D]   (encoder.rs:89-90)
     Prof p(m, st, 2, 2.0 * B * T_mel * D * 3.0 * c.n_mels * 1e-9, 4.0 * B * T_mel * (c.n_mels + D) * 1e-9);
     WA_HIP(wa::launch_conv_gelu(mel, (long)c.n_mels * T_mel, T_mel, 1, B, c.n_mels, T_mel, 1, m->conv1_wt,
@@ -788,7 +821,16 @@ wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st,
     WA_HIP(wa::launch_conv_gelu(m->h1, (long)T_mel * D, 1, D, B, D, T_mel, 2, m->conv2_wt, m->conv2_b, m->enc_pos,
                                 D, m->x, st));
   }
-  for (auto& L : m->enc) {  // EncoderBlock::forward (encoder.rs:37-49)
+  return WQ4_OK;
+}
+
+wq4_status encoder_layers(wa_model* m, int B, int l0, int l1, hipStream_t st) {
+  const Config& c = m->cfg;
+  const int D = c.n_audio_state, T = c.n_audio_ctx, H = c.n_audio_head;
+  const int64_t rows = (int64_t)B * T;
+  const double ln_gb = 8.0 * rows * D * 1e-9;
+  for (int li = l0; li < l1; ++li) {  // EncoderBlock::forward (encoder.rs:37-49)
+    const EncLayer& L = m->enc[li];
     {
       Prof p(m, st, 3, 0.0, ln_gb);
       WA_WQ4(wq4_layernorm(m->x, L.ln1_w, L.ln1_b, rows, D, m->prec, m->at_d, nullptr, st));
@@ -825,13 +867,27 @@ wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st,
       WA_WQ4(wq4_gemm_tiled(L.fc2, L.fc2_b, m->at_f, m->x, m->x, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 1, st));
     }
   }
+  return WQ4_OK;
+}
+
+wq4_status encoder_post(wa_model* m, int B, hipStream_t st, float* enc_out_f32) {
+  const Config& c = m->cfg;
+  const int D = c.n_audio_state;
+  const int64_t rows = (int64_t)B * c.n_audio_ctx;
   {
-    Prof p(m, st, 3, 0.0, ln_gb);
+    Prof p(m, st, 3, 0.0, 8.0 * rows * D * 1e-9);
     float* out = enc_out_f32 ? enc_out_f32 : m->h1;
     WA_WQ4(wq4_layernorm(m->x, m->lnp_w, m->lnp_b, rows, D, WQ4_PREC_F16X2, nullptr, out, st));
     m->enc_f32 = out;
   }
   return WQ4_OK;
+}
+
+wq4_status encoder_forward(wa_model* m, const float* mel, int B, hipStream_t st, float* enc_out_f32) {
+  wq4_status s = encoder_front(m, mel, B, st);
+  if (s == WQ4_OK) s = encoder_layers(m, B, 0, (int)m->enc.size(), st);
+  if (s == WQ4_OK) s = encoder_post(m, B, st, enc_out_f32);
+  return s;
 }
 
 // The cross-attention state of every decoder layer: the reference caches
@@ -1350,62 +1406,36 @@ wq4_status wa_prompt_logits(wa_model* m, const int32_t* prompt_dev, int n_clips,
 
 namespace {
 
-// One transcribe (whisper.rs:51-128 for a batch of clips); *overflow = the
-// range flag of this run (see wa_model::range_flag).
-wq4_status transcribe_once(wa_model* m, const float* mel_dev, int n_clips, int lang_token, int max_tokens,
-                           int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out, void* stream, bool* overflow) {
-  // all work on the model's own stream, ordered after the caller's stream
-  hipStream_t st = m->own_stream;
-  const int B = n_clips;
-  hipEvent_t ev[5];
-  for (auto& e : ev) WA_HIP(hipEventCreate(&e));
-  struct EvGuard {
-    hipEvent_t* e;
-    ~EvGuard() {
-      for (int i = 0; i < 5; ++i) (void)hipEventDestroy(e[i]);
-    }
-  } evg{ev};
-  WA_HIP(hipEventRecord(ev[4], static_cast<hipStream_t>(stream)));
-  WA_HIP(hipStreamWaitEvent(st, ev[4], 0));
-  WA_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
-
-  WA_HIP(hipEventRecord(ev[0], st));
-  wq4_status s = encoder_forward(m, mel_dev, B, st, nullptr);
-  if (s != WQ4_OK) return s;
-  WA_HIP(hipEventRecord(ev[1], st));
-  s = cross_kv_forward(m, B, st, true);
-  if (s != WQ4_OK) return s;
-  WA_HIP(hipEventRecord(ev[2], st));
-
-  // decode groups: contiguous clip ranges on their own streams, started
-  // after the encoder-planes pass, joined back into `st` at the end
-  const int G = decode_groups(B);
-  hipEvent_t kv_ready, gdone[kMaxGroups], gprompt[kMaxGroups];
-  WA_HIP(hipEventCreateWithFlags(&kv_ready, hipEventDisableTiming));
-  for (int i = 0; i < G; ++i) {
-    WA_HIP(hipEventCreate(&gdone[i]));
-    WA_HIP(hipEventCreate(&gprompt[i]));
+// HIP events destroyed with the set.
+struct EventSet {
+  std::vector<hipEvent_t> e;
+  EventSet() = default;
+  EventSet(const EventSet&) = delete;
+  EventSet& operator=(const EventSet&) = delete;
+  ~EventSet() {
+    for (hipEvent_t x : e) (void)hipEventDestroy(x);
   }
-  struct GEvGuard {
-    hipEvent_t* k;
-    hipEvent_t* d;
-    hipEvent_t* p;
-    int n;
-    ~GEvGuard() {
-      (void)hipEventDestroy(*k);
-      for (int i = 0; i < n; ++i) {
-        (void)hipEventDestroy(d[i]);
-        (void)hipEventDestroy(p[i]);
-      }
-    }
-  } geg{&kv_ready, gdone, gprompt, G};
-  WA_HIP(hipEventRecord(kv_ready, st));
+  hipError_t make(hipEvent_t* out, bool timing = true) {
+    hipError_t r = hipEventCreateWithFlags(out, timing ? hipEventDefault : hipEventDisableTiming);
+    if (r == hipSuccess) e.push_back(*out);
+    return r;
+  }
+};
+
+// Prompt + greedy loop (whisper.rs:60-125) of every decode group of a batch
+// of B clips, each group's stream first waiting on `ready` (the encoder
+// planes of the batch).  Records gprompt[i] after group i's prompt and
+// gdone[i] after its last step; the host blocks only for the lagged EOT
+// polls (eot_stop).
+wq4_status run_decode(wa_model* m, int B, int lang_token, int max_tokens, int eot_stop, hipEvent_t ready,
+                      const hipEvent_t* gprompt, const hipEvent_t* gdone, int* steps_out) {
+  const int G = decode_groups(B);
   for (int i = 0; i < G; ++i) {
     DecGroup& g = m->groups[i];
     g.b0 = (int)((int64_t)B * i / G);
     g.nb = (int)((int64_t)B * (i + 1) / G) - g.b0;
-    WA_HIP(hipStreamWaitEvent(g.st, kv_ready, 0));
-    s = prompt_group(m, g, lang_token, g.st);
+    WA_HIP(hipStreamWaitEvent(g.st, ready, 0));
+    wq4_status s = prompt_group(m, g, lang_token, g.st);
     if (s != WQ4_OK) return s;
     WA_HIP(hipEventRecord(gprompt[i], g.st));
     s = ensure_graph(m, g, eot_stop);
@@ -1413,17 +1443,11 @@ wq4_status transcribe_once(wa_model* m, const float* mel_dev, int n_clips, int l
   }
   // greedy loop (whisper.rs:104-125): each step replays every live group's
   // graph; a group stops once all its clips emitted EOT (polled with a lag)
+  EventSet ev;
   hipEvent_t ring[kMaxGroups][8];
-  for (int i = 0; i < G; ++i)
-    for (auto& e : ring[i]) WA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  struct RingGuard {
-    hipEvent_t (*e)[8];
-    int n;
-    ~RingGuard() {
-      for (int i = 0; i < n; ++i)
-        for (int j = 0; j < 8; ++j) (void)hipEventDestroy(e[i][j]);
-    }
-  } rg{ring, G};
+  if (eot_stop)
+    for (int i = 0; i < G; ++i)
+      for (auto& e : ring[i]) WA_HIP(ev.make(&e, false));
   int steps = 0;
   const int lag = 4;
   bool live[kMaxGroups] = {};
@@ -1455,41 +1479,249 @@ wq4_status transcribe_once(wa_model* m, const float* mel_dev, int n_clips, int l
   }
   // the loop's bookkeeping for tokens chosen by the last step happens at the
   // top of a step that the reference never runs: nothing to add.
-  for (int i = 0; i < G; ++i) {
-    WA_HIP(hipEventRecord(gdone[i], m->groups[i].st));
-    WA_HIP(hipStreamWaitEvent(st, gdone[i], 0));
-  }
-  WA_HIP(hipEventRecord(ev[4], st));
-  std::vector<int32_t> tok((size_t)B * kMaxTokens), nt(B);
+  for (int i = 0; i < G; ++i) WA_HIP(hipEventRecord(gdone[i], m->groups[i].st));
+  *steps_out = steps;
+  return WQ4_OK;
+}
+
+// `st` waits for every group of the batch, then copies the groups' tokens /
+// counts (kMaxTokens per clip) and the range flag to (pinned) host memory.
+wq4_status collect_batch(wa_model* m, int B, const hipEvent_t* gdone, hipStream_t st, int32_t* tok, int32_t* nt,
+                         int* flag) {
+  const int G = decode_groups(B);
+  for (int i = 0; i < G; ++i) WA_HIP(hipStreamWaitEvent(st, gdone[i], 0));
   for (int i = 0; i < G; ++i) {
     const DecGroup& g = m->groups[i];
-    WA_HIP(hipMemcpyAsync(tok.data() + (size_t)g.b0 * kMaxTokens, g.tokens, (size_t)g.nb * kMaxTokens * 4,
+    WA_HIP(hipMemcpyAsync(tok + (size_t)g.b0 * kMaxTokens, g.tokens, (size_t)g.nb * kMaxTokens * 4,
                           hipMemcpyDeviceToHost, st));
-    WA_HIP(hipMemcpyAsync(nt.data() + g.b0, g.ntok, (size_t)g.nb * 4, hipMemcpyDeviceToHost, st));
+    WA_HIP(hipMemcpyAsync(nt + g.b0, g.ntok, (size_t)g.nb * 4, hipMemcpyDeviceToHost, st));
   }
-  int flag = 0;
-  WA_HIP(hipMemcpyAsync(&flag, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
-  WA_HIP(hipStreamSynchronize(st));
-  *overflow = flag != 0;
+  WA_HIP(hipMemcpyAsync(flag, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+  return WQ4_OK;
+}
+
+void copy_tokens(const int32_t* tok, const int32_t* nt, int B, int max_tokens, int32_t* tokens_out,
+                 int32_t* n_tokens_out) {
   for (int b = 0; b < B; ++b) {
     n_tokens_out[b] = std::min(nt[b], max_tokens);
-    std::memcpy(tokens_out + (size_t)b * max_tokens, tok.data() + (size_t)b * kMaxTokens,
-                (size_t)max_tokens * 4);
+    std::memcpy(tokens_out + (size_t)b * max_tokens, tok + (size_t)b * kMaxTokens, (size_t)max_tokens * 4);
   }
+}
+
+// One transcribe (whisper.rs:51-128 for a batch of clips); *overflow = the
+// range flag of this run (see wa_model::range_flag).
+wq4_status transcribe_once(wa_model* m, const float* mel_dev, int n_clips, int lang_token, int max_tokens,
+                           int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out, void* stream, bool* overflow) {
+  // all work on the model's own stream, ordered after the caller's stream
+  hipStream_t st = m->own_stream;
+  const int B = n_clips;
+  const int G = decode_groups(B);
+  EventSet ev;
+  hipEvent_t e_in, e_enc, e_kv, e_ready, e_end, gprompt[kMaxGroups], gdone[kMaxGroups];
+  for (hipEvent_t* e : {&e_in, &e_enc, &e_kv, &e_ready, &e_end}) WA_HIP(ev.make(e));
+  for (int i = 0; i < G; ++i) {
+    WA_HIP(ev.make(&gprompt[i]));
+    WA_HIP(ev.make(&gdone[i]));
+  }
+  WA_HIP(hipEventRecord(e_in, static_cast<hipStream_t>(stream)));
+  WA_HIP(hipStreamWaitEvent(st, e_in, 0));
+  WA_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
+
+  WA_HIP(hipEventRecord(e_enc, st));
+  wq4_status s = encoder_forward(m, mel_dev, B, st, nullptr);
+  if (s != WQ4_OK) return s;
+  WA_HIP(hipEventRecord(e_kv, st));
+  s = cross_kv_forward(m, B, st, true);
+  if (s != WQ4_OK) return s;
+  WA_HIP(hipEventRecord(e_ready, st));
+  // decode groups: contiguous clip ranges on their own streams, started
+  // after the encoder-planes pass, joined back into `st` at the end
+  int steps = 0;
+  s = run_decode(m, B, lang_token, max_tokens, eot_stop, e_ready, gprompt, gdone, &steps);
+  if (s != WQ4_OK) return s;
+  std::vector<int32_t> tok((size_t)B * kMaxTokens), nt(B);
+  int flag = 0;
+  s = collect_batch(m, B, gdone, st, tok.data(), nt.data(), &flag);
+  if (s != WQ4_OK) return s;
+  WA_HIP(hipEventRecord(e_end, st));
+  WA_HIP(hipStreamSynchronize(st));
+  *overflow = flag != 0;
+  copy_tokens(tok.data(), nt.data(), B, max_tokens, tokens_out, n_tokens_out);
   // phases: encoder, encoder planes (the cross-attention state), prompt (slowest group), decode loop
-  float ms[3], tp = 0.0f, tall = 0.0f;
-  for (int i = 0; i < 2; ++i) WA_HIP(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
+  float t_enc = 0.0f, t_kv = 0.0f, tp = 0.0f, tall = 0.0f;
+  WA_HIP(hipEventElapsedTime(&t_enc, e_enc, e_kv));
+  WA_HIP(hipEventElapsedTime(&t_kv, e_kv, e_ready));
   for (int i = 0; i < G; ++i) {
     float t = 0.0f;
-    WA_HIP(hipEventElapsedTime(&t, ev[2], gprompt[i]));
+    WA_HIP(hipEventElapsedTime(&t, e_ready, gprompt[i]));
     tp = std::max(tp, t);
   }
-  WA_HIP(hipEventElapsedTime(&tall, ev[2], ev[4]));
-  m->timings[0] = ms[0];
-  m->timings[1] = ms[1];
+  WA_HIP(hipEventElapsedTime(&tall, e_ready, e_end));
+  m->timings[0] = t_enc;
+  m->timings[1] = t_kv;
   m->timings[2] = tp;
   m->timings[3] = tall - tp;
   m->timings[4] = (float)steps;
+  return WQ4_OK;
+}
+
+// The CU-masked stream of the pipelined transcribe's overlapped encoder
+// part: bits 0 .. n-1 of the mask, which the driver spreads over the XCDs
+// (bit i -> XCD i mod 8), n / 8 CUs of each; created on first use.
+wq4_status ensure_enc_stream(wa_model* m) {
+  if (m->enc_stream) return WQ4_OK;
+  hipDeviceProp_t prop;
+  WA_HIP(hipGetDeviceProperties(&prop, m->device));
+  const int total = prop.multiProcessorCount;
+  int n = kEncOverlapCUs;
+  if (const char* e = getenv("WA_ENC_CUS")) n = atoi(e);
+  n = std::max(8, std::min(total, n));
+  std::vector<uint32_t> mask((total + 31) / 32, 0u);
+  for (int i = 0; i < n; ++i) mask[i / 32] |= 1u << (i % 32);
+  WA_HIP(hipExtStreamCreateWithCUMask(&m->enc_stream, (uint32_t)mask.size(), mask.data()));
+  m->enc_cus = n;
+  return WQ4_OK;
+}
+
+// wa_transcribe over n_batches batches of n_clips clips, software-pipelined:
+// while batch i decodes (its groups' streams), the conv stem and the first
+// k encoder layers of batch i + 1 run on the CU-masked stream (a few CUs of
+// every XCD; the decode keeps the rest), and once batch i's decode is done
+// the remaining layers, ln_post and the encoder planes of batch i + 1 run
+// at full width on the model stream.  The encoder buffers are free during a
+// decode (it reads only the planes, rewritten after the decode it serves),
+// so nothing is double-buffered.  k adapts per batch to the last decode's
+// length over the masked stream's measured time per layer.  Every kernel
+// computes what it computes in wa_transcribe: the same tokens.  flags[i] =
+// batch i's range flag (the caller re-runs flagged batches).
+wq4_status transcribe_pipelined(wa_model* m, const float* mel_dev, int NB, int B, int lang_token, int max_tokens,
+                                int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out, void* stream, int* flags) {
+  WA_WQ4(ensure_enc_stream(m));
+  hipStream_t st = m->own_stream, es = m->enc_stream;
+  const int L = (int)m->enc.size(), G = decode_groups(B);
+  const size_t mel_stride = (size_t)B * m->cfg.n_mels * 2 * m->cfg.n_audio_ctx;
+  // pinned result staging: per batch the groups' tokens, counts and range flag
+  int32_t* host = nullptr;
+  const size_t per = (size_t)B * kMaxTokens + B + 1;
+  WA_HIP(hipHostMalloc(reinterpret_cast<void**>(&host), (size_t)NB * per * 4, 0));
+  struct HostGuard {
+    int32_t* p;
+    ~HostGuard() { (void)hipHostFree(p); }
+  } hg{host};
+  EventSet ev;
+  struct Batch {
+    hipEvent_t ready, mstart, mend, pstart, gprompt[kMaxGroups], gdone[kMaxGroups];
+    int k = 0, steps = 0;
+  };
+  std::vector<Batch> bt(NB);
+  for (Batch& b : bt) {
+    for (hipEvent_t* e : {&b.ready, &b.mstart, &b.mend, &b.pstart}) WA_HIP(ev.make(e));
+    for (int i = 0; i < G; ++i) {
+      WA_HIP(ev.make(&b.gprompt[i]));
+      WA_HIP(ev.make(&b.gdone[i]));
+    }
+  }
+  hipEvent_t e_in, e_enc0;
+  WA_HIP(ev.make(&e_in));
+  WA_HIP(ev.make(&e_enc0));
+  WA_HIP(hipEventRecord(e_in, static_cast<hipStream_t>(stream)));
+  WA_HIP(hipStreamWaitEvent(st, e_in, 0));
+  // batch 0: the whole encoder at full width
+  WA_HIP(hipEventRecord(e_enc0, st));
+  wq4_status s = encoder_forward(m, mel_dev, B, st, nullptr);
+  if (s == WQ4_OK) s = cross_kv_forward(m, B, st, true);
+  if (s != WQ4_OK) return s;
+  WA_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
+  WA_HIP(hipEventRecord(bt[0].ready, st));
+  if (m->overlap_k < 0) m->overlap_k = std::min(L, kEncOverlapLayers0);
+  double t_exposed = 0.0, t_masked = 0.0, t_decode = 0.0, t_prompt = 0.0, k_sum = 0.0;
+  int32_t steps_all = 0;
+  for (int i = 0; i < NB; ++i) {
+    Batch& b = bt[i];
+    if (i >= 1) {
+      // batch i - 1 is decoded (and batch i's masked part done) before batch
+      // i's decode is enqueued: the GPU meanwhile runs batch i's remaining
+      // layers; adapt k to the finished decode
+      Batch& p = bt[i - 1];
+      for (int g = 0; g < G; ++g) WA_HIP(hipEventSynchronize(p.gdone[g]));
+      WA_HIP(hipEventSynchronize(p.mend));
+      float td = 0.0f, tm = 0.0f;
+      for (int g = 0; g < G; ++g) {
+        float t = 0.0f;
+        WA_HIP(hipEventElapsedTime(&t, p.ready, p.gdone[g]));
+        td = std::max(td, t);
+      }
+      WA_HIP(hipEventElapsedTime(&tm, p.mstart, p.mend));
+      if (!getenv("WA_ENC_OVERLAP")) {
+        const double per_layer = tm / (double)(p.k + 1);  // the conv stem counts as one layer
+        m->overlap_k = std::max(0, std::min(L, (int)(kEncOverlapFill * td / per_layer) - 1));
+      }
+    }
+    if (const char* e = getenv("WA_ENC_OVERLAP")) m->overlap_k = std::max(0, std::min(L, atoi(e)));
+    if (i + 1 < NB) {  // the masked part of batch i + 1, beside batch i's decode
+      b.k = m->overlap_k;
+      WA_HIP(hipStreamWaitEvent(es, b.ready, 0));
+      WA_HIP(hipEventRecord(b.mstart, es));
+      s = encoder_front(m, mel_dev + (i + 1) * mel_stride, B, es);
+      if (s == WQ4_OK) s = encoder_layers(m, B, 0, b.k, es);
+      if (s != WQ4_OK) return s;
+      WA_HIP(hipEventRecord(b.mend, es));
+    }
+    s = run_decode(m, B, lang_token, max_tokens, eot_stop, b.ready, b.gprompt, b.gdone, &b.steps);
+    if (s != WQ4_OK) return s;
+    int32_t* hb = host + (size_t)i * per;
+    s = collect_batch(m, B, b.gdone, st, hb, hb + (size_t)B * kMaxTokens, hb + (size_t)B * kMaxTokens + B);
+    if (s != WQ4_OK) return s;
+    if (i + 1 < NB) {  // the rest of batch i + 1's encoder at full width
+      WA_HIP(hipStreamWaitEvent(st, b.mend, 0));
+      WA_HIP(hipEventRecord(b.pstart, st));
+      s = encoder_layers(m, B, b.k, L, st);
+      if (s == WQ4_OK) s = encoder_post(m, B, st, nullptr);
+      if (s == WQ4_OK) s = cross_kv_forward(m, B, st, true);
+      if (s != WQ4_OK) return s;
+      WA_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
+      WA_HIP(hipEventRecord(bt[i + 1].ready, st));
+    }
+  }
+  WA_HIP(hipStreamSynchronize(st));
+  for (int i = 0; i < NB; ++i) {
+    const int32_t* hb = host + (size_t)i * per;
+    copy_tokens(hb, hb + (size_t)B * kMaxTokens, B, max_tokens, tokens_out + (size_t)i * B * max_tokens,
+                n_tokens_out + (size_t)i * B);
+    flags[i] = hb[(size_t)B * kMaxTokens + B];
+    // per-batch phases (averaged below)
+    Batch& b = bt[i];
+    float t = 0.0f, tp = 0.0f, td = 0.0f;
+    if (i == 0) {
+      WA_HIP(hipEventElapsedTime(&t, e_enc0, b.ready));
+    } else {
+      WA_HIP(hipEventElapsedTime(&t, bt[i - 1].pstart, b.ready));
+      float tm = 0.0f;
+      WA_HIP(hipEventElapsedTime(&tm, bt[i - 1].mstart, bt[i - 1].mend));
+      t_masked += tm;
+      k_sum += bt[i - 1].k;
+    }
+    t_exposed += t;
+    for (int g = 0; g < G; ++g) {
+      float a = 0.0f, d = 0.0f;
+      WA_HIP(hipEventElapsedTime(&a, b.ready, b.gprompt[g]));
+      WA_HIP(hipEventElapsedTime(&d, b.ready, b.gdone[g]));
+      tp = std::max(tp, a);
+      td = std::max(td, d);
+    }
+    t_prompt += tp;
+    t_decode += td - tp;
+    steps_all += b.steps;
+  }
+  m->timings[0] = (float)(t_exposed / NB);
+  m->timings[1] = 0.0f;
+  m->timings[2] = (float)(t_prompt / NB);
+  m->timings[3] = (float)(t_decode / NB);
+  m->timings[4] = (float)steps_all / NB;
+  m->pipe[0] = (float)NB;
+  m->pipe[1] = NB > 1 ? (float)(k_sum / (NB - 1)) : 0.0f;
+  m->pipe[2] = NB > 1 ? (float)(t_masked / (NB - 1)) : 0.0f;
+  m->pipe[3] = (float)m->enc_cus;
   return WQ4_OK;
 }
 
@@ -1530,6 +1762,35 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
     return fail(WQ4_ERANGE,
                 "activation overflow: an MFMA operand left the f16-pair range (|x| >= 4094 after the LayerNorm, "
                 "GELU or attention producers) and the logits are not finite");
+  return WQ4_OK;
+}
+
+wq4_status wa_transcribe_batches(wa_model* m, const float* mel_dev, int n_batches, int n_clips, int lang_token,
+                                 int max_tokens, int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out,
+                                 void* stream) {
+  if (!m || !mel_dev || !tokens_out || !n_tokens_out) return fail(WQ4_EINVAL, "null argument");
+  if (n_batches < 1) return fail(WQ4_EINVAL, "n_batches must be >= 1");
+  if (n_clips < 1 || n_clips > m->bmax) return fail(WQ4_EINVAL, "n_clips out of range");
+  if (max_tokens < 1 || max_tokens > kMaxTokens) return fail(WQ4_EINVAL, "max_tokens must be in [1, 224]");
+  WA_HIP(hipSetDevice(m->device));
+  std::vector<int> flags(n_batches, 0);
+  wq4_status s = transcribe_pipelined(m, mel_dev, n_batches, n_clips, lang_token, max_tokens, eot_stop, tokens_out,
+                                      n_tokens_out, stream, flags.data());
+  if (s != WQ4_OK) return s;
+  const size_t mel_stride = (size_t)n_clips * m->cfg.n_mels * 2 * m->cfg.n_audio_ctx;
+  for (int i = 0; i < n_batches; ++i) {
+    if (!flags[i]) continue;
+    // a flagged batch goes through wa_transcribe's range tiers on its own
+    s = wa_transcribe(m, mel_dev + i * mel_stride, n_clips, lang_token, max_tokens, eot_stop,
+                      tokens_out + (size_t)i * n_clips * max_tokens, n_tokens_out + (size_t)i * n_clips, stream);
+    if (s != WQ4_OK) return s;
+  }
+  return WQ4_OK;
+}
+
+wq4_status wa_last_pipeline_stats(const wa_model* m, float* out) {
+  if (!m || !out) return fail(WQ4_EINVAL, "null argument");
+  std::memcpy(out, m->pipe, sizeof(m->pipe));
   return WQ4_OK;
 }
 

@@ -41,6 +41,8 @@ def lib() -> ctypes.CDLL:
         L.wa_model_device_bytes.restype = ctypes.c_size_t
         L.wa_transcribe.argtypes = [vp, vp, c_int, c_int, c_int, c_int, i32p, i32p, vp]
         L.wa_last_timings.argtypes = [vp, f32p]
+        L.wa_transcribe_batches.argtypes = [vp, vp, c_int, c_int, c_int, c_int, c_int, i32p, i32p, vp]
+        L.wa_last_pipeline_stats.argtypes = [vp, f32p]
         L.wa_encode.argtypes = [vp, vp, c_int, vp, vp]
         L.wa_prompt_logits.argtypes = [vp, vp, c_int, c_int, vp, vp]
         L.wa_synth_uniform.argtypes = [ctypes.c_uint64, ctypes.c_char_p, c_i64, ctypes.c_float, ctypes.c_float, f32p]
@@ -76,7 +78,8 @@ def lib() -> ctypes.CDLL:
         L.wa_self_attention_check.argtypes = [c_int, vp, vp, vp, c_int, c_int, c_int, c_int, c_int, c_int, vp]
         L.wa_logits_argmax_check.argtypes = [c_int, vp, vp, c_int, c_int, c_int, c_int, c_int, vp, vp]
         for n in ("wa_xattn_check", "wa_xattn_kv_check", "wa_transcribe_trace", "wa_encoder_attention_check", "wa_self_attention_check",
-                  "wa_logits_argmax_check", "wa_log_mel", "wa_mel_filterbank", "wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_last_timings", "wa_encode",
+                  "wa_logits_argmax_check", "wa_log_mel", "wa_mel_filterbank", "wa_model_create_synthetic", "wa_model_config", "wa_transcribe", "wa_transcribe_batches",
+                  "wa_last_pipeline_stats", "wa_last_timings", "wa_encode",
                   "wa_prompt_logits", "wa_synth_uniform", "wa_profile_enable", "wa_profile_read", "wa_probe_kernels",
                   "wa_decode_group_rows",
                   "wa_model_create_from_gguf", "wa_model_create_synthetic_ex", "wa_gguf_open", "wa_gguf_tensor_info", "wa_gguf_tensor_data"):
@@ -322,6 +325,31 @@ class WhisperModel:
                                   -1 if lang_token is None else int(lang_token), max_tokens, 1 if eot_stop else 0,
                                   toks.ctypes.data_as(i32p), nt.ctypes.data_as(i32p), self._stream()))
         return [toks[b, : nt[b]].tolist() for b in range(B)]
+
+    def transcribe_batches(self, mels, lang_token: Optional[int] = 50259, max_tokens: int = 224,
+                           eot_stop: bool = True):
+        """transcribe over mels cuda f32 [NB, B, n_mels, 3000], the next batch's
+        encoder pipelined beside each decode (wa_transcribe_batches).  Returns
+        NB lists of B token-id lists."""
+        torch = _torch()
+        mels = mels.contiguous()
+        assert mels.dtype == torch.float32 and mels.is_cuda and mels.dim() == 4
+        NB, B = mels.shape[0], mels.shape[1]
+        toks = np.zeros((NB, B, max_tokens), np.int32)
+        nt = np.zeros((NB, B), np.int32)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        check(lib().wa_transcribe_batches(self._h, ctypes.c_void_p(mels.data_ptr()), NB, B,
+                                          -1 if lang_token is None else int(lang_token), max_tokens,
+                                          1 if eot_stop else 0, toks.ctypes.data_as(i32p), nt.ctypes.data_as(i32p),
+                                          self._stream()))
+        return [[toks[i, b, : nt[i, b]].tolist() for b in range(B)] for i in range(NB)]
+
+    def pipeline_stats(self) -> dict:
+        """After transcribe_batches: batches, mean encoder layers run beside a
+        decode, mean ms of that CU-masked part, CUs of the masked stream."""
+        t = (ctypes.c_float * 4)()
+        check(lib().wa_last_pipeline_stats(self._h, t))
+        return {"batches": int(t[0]), "overlap_layers": t[1], "masked_ms": t[2], "masked_cus": int(t[3])}
 
     def transcribe_trace(self, mel, trace_ids: np.ndarray, lang_token: Optional[int] = 50259,
                          max_tokens: int = 224, eot_stop: bool = False):
