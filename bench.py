@@ -492,9 +492,10 @@ def main() -> None:
     pipelined = not args.audio and not args.sequential
     eot = not args.fixed_length
     if pipelined:
-        warm = torch.stack(inputs[: args.warmup] if args.warmup >= 2 else [inputs[0], inputs[0]])
-        model.transcribe_batches(warm, lang, args.max_tokens, eot_stop=eot)  # graphs, masked stream, overlap depth
-        del warm
+        if args.warmup > 0:  # graphs, the masked stream and the overlap depth (a 1-step warmup runs 2 batches)
+            warm = torch.stack(inputs[: args.warmup] if args.warmup >= 2 else [inputs[0], inputs[0]])
+            model.transcribe_batches(warm, lang, args.max_tokens, eot_stop=eot)
+            del warm
         timed_in = torch.stack(inputs[args.warmup:])
     else:
         for s in range(args.warmup):
