@@ -259,8 +259,9 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   __shared__ __attribute__((aligned(16))) _Float16 sp[NS][32][kTc + 8];  // row stride 12 dwords: conflict-free P reads
   __shared__ float salpha[32];
   __shared__ int srescale[2];
-  __shared__ __attribute__((aligned(16))) _Float16 szero[8];
-  __shared__ __attribute__((aligned(16))) _Float16 sq1[HT == 2 ? NS : 1][4][HT == 2 ? D + 16 : 8];
+  // heads 16..19 (H in (16, 20]) in rows 0..3, row 4 zeros: the padding lanes
+  // of the second head tile read row 4 at the same immediate offsets
+  __shared__ __attribute__((aligned(16))) _Float16 sq1[HT == 2 ? NS : 1][5][HT == 2 ? D + 16 : 8];
 
   const int s = blockIdx.x, r = blockIdx.y;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -294,17 +295,16 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
         qb[ht][ks][p] = *reinterpret_cast<const half8*>(
             qt + (((size_t)r * NS + p) * HP + ht * 16 + l16) * D + c0 + ks * 32 + 8 * lq);
   if (HT == 2) {
-    for (int i = tid; i < NS * 4 * (D / 8); i += kThreads) {
-      const int p = i / (4 * (D / 8)), rem = i - p * 4 * (D / 8), hr = rem / (D / 8), c8 = rem - hr * (D / 8);
+    for (int i = tid; i < NS * 5 * (D / 8); i += kThreads) {
+      const int p = i / (5 * (D / 8)), rem = i - p * 5 * (D / 8), hr = rem / (D / 8), c8 = rem - hr * (D / 8);
       *reinterpret_cast<half8*>(&sq1[p][hr][8 * c8]) =
-          *reinterpret_cast<const half8*>(qt + (((size_t)r * NS + p) * HP + 16 + hr) * D + 8 * c8);
+          hr < 4 ? *reinterpret_cast<const half8*>(qt + (((size_t)r * NS + p) * HP + 16 + hr) * D + 8 * c8) : half8{};
     }
   }
   // rows of P past the score tiles stay 0, their alpha 1
   for (int i = tid; i < NS * 32 * (kTc + 8); i += kThreads) (&sp[0][0][0])[i] = (_Float16)(WA_XATTN_DIAG == 9 ? 1.0f : 0.0f);
   if (tid < 32) salpha[tid] = 1.0f;
   if (tid < 2) srescale[tid] = 0;
-  if (tid < 8) szero[tid] = (_Float16)0.0f;
 
   floatx16 zacc[KS];
 #pragma unroll
@@ -370,26 +370,27 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
 
   // scores of this wave's column slice: A = enc (m = frame, k = column) from
   // afrag(ks, plane), B = qt (k = column, n = head); partial sums to red
+  const int q1row = l16 < 4 ? l16 : 4;
+  auto b1frag = [&](int ks, int p) {  // heads 16..19; the padding lanes read the zero row (no exec branch)
+    return *reinterpret_cast<const half8*>(&sq1[p][q1row][c0 + ks * 32 + 8 * lq]);
+  };
   auto scores = [&](auto&& afrag) {
     floatx4 sacc[HT];
 #pragma unroll
     for (int ht = 0; ht < HT; ++ht) sacc[ht] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int ks = 0; ks < (WA_XATTN_DIAG == 3 ? 0 : KS); ++ks) {
-      half8 a[NS];
+      half8 a[NS], b1[NS];
 #pragma unroll
-      for (int p = 0; p < NS; ++p) a[p] = afrag(ks, p);
+      for (int p = 0; p < NS; ++p) {
+        a[p] = afrag(ks, p);
+        if (HT > HR) b1[p] = b1frag(ks, p);
+      }
 #pragma unroll
       for (int ht = 0; ht < HT; ++ht) {
         half8 b[NS];
 #pragma unroll
-        for (int p = 0; p < NS; ++p) {
-          if (ht < HR) {
-            b[p] = qb[ht < HR ? ht : 0][ks][p];
-          } else {  // heads 16..19; the padding lanes read a zero fragment (no exec branch)
-            b[p] = *reinterpret_cast<const half8*>(l16 < 4 ? &sq1[p][l16 & 3][c0 + ks * 32 + 8 * lq] : szero);
-          }
-        }
+        for (int p = 0; p < NS; ++p) b[p] = ht < HR ? qb[ht < HR ? ht : 0][ks][p] : b1[p];
         sacc[ht] = mfma16x32(a[0], b[0], sacc[ht]);
         if constexpr (NS == 2) {
           sacc[ht] = mfma16x32(a[1], b[0], sacc[ht]);
@@ -487,7 +488,7 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
   u32x4v pre0[NLD];
   u32x4v pre1[PF == 2 ? NLD : 1];
   if (nch > 0) fetch(pre0, 0);
-  __syncthreads();  // sq1, sp, salpha, srescale, szero initialised
+  __syncthreads();  // sq1, sp, salpha, srescale initialised
   if constexpr (PF == 2) {
     if (nch > 1) fetch(pre1, 1);
     for (int chi = 0; chi < nch; chi += 2) {
