@@ -741,20 +741,7 @@ wq4_status alloc_activations(wa_model* m) {
     WA_HIP(hipMemset(g.atd_dec, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
     WA_HIP(hipMemset(g.atf_dec, 0, wq4_atiled_bytes(rdec, Ft, m->prec)));
     WA_HIP(hipHostMalloc(reinterpret_cast<void**>(&g.host_ndone), 8 * sizeof(int), 0));
-    if (const char* e = getenv("WA_DECODE_CUMASK"); e && atoi(e) > 0) {  // A/B: decode off the encoder's first n CUs
-      hipDeviceProp_t prop;
-      WA_HIP(hipGetDeviceProperties(&prop, m->device));
-      const int total = prop.multiProcessorCount;
-      std::vector<uint32_t> mask((total + 31) / 32, 0u);
-      for (int i = atoi(e); i < total; ++i) mask[i / 32] |= 1u << (i % 32);
-      WA_HIP(hipExtStreamCreateWithCUMask(&g.st, (uint32_t)mask.size(), mask.data()));
-    } else if (const char* e = getenv("WA_GROUP_PRIO"); e && atoi(e) != 0) {  // A/B probe (scripts/encode_overlap_probe.py)
-      int lo = 0, hi = 0;
-      WA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      WA_HIP(hipStreamCreateWithPriority(&g.st, hipStreamNonBlocking, atoi(e) > 0 ? hi : lo));
-    } else {
-      WA_HIP(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
-    }
+    WA_HIP(hipStreamCreateWithFlags(&g.st, hipStreamNonBlocking));
   }
   m->range_flag = d.alloc<int>(1);
   for (void* p : {(void*)m->h1, (void*)m->x, (void*)m->qkv, (void*)m->at_d, (void*)m->at_f, (void*)m->enc_planes,
