@@ -211,15 +211,6 @@ struct DecGroup {
   int* host_ndone = nullptr;  // pinned ring
   hipGraphExec_t graph = nullptr;
   int64_t graph_key = -1;  // (b0, nb, eot mode, trace) the graph was captured for
-  // the prompt (prompt_group) as a graph of its own: device copies of the
-  // prompt tokens (uploaded when the language or the clip count changes),
-  // of SOT per clip and of the two DecodeStates a prompt ends in
-  int* prompt_init = nullptr;
-  int* sot_init = nullptr;
-  wa::DecodeState* state_init = nullptr;  // [0] explicit language, [1] auto
-  int prompt_lang = -2, prompt_nb = -1;
-  hipGraphExec_t pgraph = nullptr;
-  int64_t pgraph_key = -1;
 };
 
 }  // namespace
@@ -322,7 +313,6 @@ struct wa_model {
     resolve_profile();
     for (auto& g : groups) {
       if (g.graph) (void)hipGraphExecDestroy(g.graph);
-      if (g.pgraph) (void)hipGraphExecDestroy(g.pgraph);
       if (g.st) (void)hipStreamDestroy(g.st);
       if (g.host_ndone) (void)hipHostFree(g.host_ndone);
     }
@@ -720,9 +710,6 @@ wq4_status alloc_activations(wa_model* m) {
     g.atd_dec = tiled(rdec, Dt);
     g.atf_dec = tiled(rdec, Ft);
     g.prompt_tok = d.alloc<int>(rdec);
-    g.prompt_init = d.alloc<int>(rdec);
-    g.sot_init = d.alloc<int>(B);
-    g.state_init = d.alloc<wa::DecodeState>(2);
     g.next_tok = d.alloc<int>(B);
     g.tokens = d.alloc<int>((size_t)B * kMaxTokens);
     g.ntok = d.alloc<int>(B);
@@ -744,17 +731,8 @@ wq4_status alloc_activations(wa_model* m) {
                     (void*)g.atf_dec, (void*)g.prompt_tok, (void*)g.next_tok, (void*)g.tokens, (void*)g.ntok,
                     (void*)g.done, (void*)g.state, (void*)g.xattn_part, (void*)g.xqt, (void*)g.lg_val,
                     (void*)g.lg_idx, (void*)g.lg_ctr, (void*)g.atd_ln, (void*)g.ln_stats, (void*)g.hid_t,
-                    (void*)g.xkv_part, (void*)g.xkv_ctr, (void*)g.prompt_init, (void*)g.sot_init,
-                    (void*)g.state_init})
+                    (void*)g.xkv_part, (void*)g.xkv_ctr})
       if (!p) return fail(WQ4_ENOMEM, "decode-group allocation failed");
-    {
-      // whisper.rs:60-99: an explicit-language prompt leaves position 4 and
-      // 4 cached keys; the auto-language one position 4 and 3 keys
-      const wa::DecodeState init[2] = {{3, 3, -1, 0}, {3, 2, -1, 0}};
-      WA_HIP(hipMemcpy(g.state_init, init, sizeof(init), hipMemcpyHostToDevice));
-      std::vector<int> sot(B, kSOT);
-      WA_HIP(hipMemcpy(g.sot_init, sot.data(), (size_t)B * 4, hipMemcpyHostToDevice));
-    }
     WA_HIP(hipMemset(g.xkv_ctr, 0, (size_t)kvc * c.n_text_head * sizeof(int)));
     WA_HIP(hipMemset(g.atd_ln, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));
     WA_HIP(hipMemset(g.hid_t, 0, wq4_atiled_bytes(rdec, Dt, m->prec)));  // padded clips stay 0
@@ -1089,24 +1067,38 @@ wq4_status decode_step(wa_model* m, DecGroup& g, int eot_stop, hipStream_t st) {
 }
 
 // Prompt of group g (whisper.rs:60-99), leaving the first greedy token in
-// next_tok and the DecodeState ready for the step graph.  Every operand is
-// already on the device (prompt_init, sot_init, state_init), so the whole
-// prompt is a replayable graph (prompt_graph).
-wq4_status prompt_body(wa_model* m, DecGroup& g, bool explicit_lang, hipStream_t st) {
+// next_tok and the DecodeState ready for the step graph.
+wq4_status prompt_group(wa_model* m, DecGroup& g, int lang_token, hipStream_t st) {
   const Config& c = m->cfg;
   const int B = g.nb;
-  const int plen = explicit_lang ? 4 : 3;
-  WA_HIP(hipMemcpyAsync(g.prompt_tok, g.prompt_init, (size_t)B * plen * 4, hipMemcpyDeviceToDevice, st));
+  std::vector<int> ptok((size_t)B * 4);
+  int pos0, kv0;
   wq4_status s;
-  if (explicit_lang) {
+  if (lang_token >= 0) {
+    for (int b = 0; b < B; ++b) {
+      ptok[b * 4 + 0] = kSOT;
+      ptok[b * 4 + 1] = lang_token;
+      ptok[b * 4 + 2] = c.transcribe_token();
+      ptok[b * 4 + 3] = c.no_timestamps_token();
+    }
+    WA_HIP(hipMemcpyAsync(g.prompt_tok, ptok.data(), (size_t)B * 4 * 4, hipMemcpyHostToDevice, st));
     s = decoder_forward(m, g, g.prompt_tok, 4, nullptr, 0, 0, st);
     if (s != WQ4_OK) return s;
+    pos0 = 4;
+    kv0 = 4;
   } else {
     // decode_step(SOT, 0) fills a 1-entry cache; the language is the last max
     // over the language-token range (whisper.rs:73-83) ...
+    for (int b = 0; b < B; ++b) {
+      ptok[b * 3 + 0] = kSOT;
+      ptok[b * 3 + 1] = c.transcribe_token();
+      ptok[b * 3 + 2] = c.no_timestamps_token();
+    }
+    WA_HIP(hipMemcpyAsync(g.prompt_tok, ptok.data(), (size_t)B * 3 * 4, hipMemcpyHostToDevice, st));
     // SOT rows: embed reads tokens[b * Tq + t] with Tq = 1 -> a contiguous [B]
     // array: next_tok as scratch
-    WA_HIP(hipMemcpyAsync(g.next_tok, g.sot_init, (size_t)B * 4, hipMemcpyDeviceToDevice, st));
+    std::vector<int> sot(B, kSOT);
+    WA_HIP(hipMemcpyAsync(g.next_tok, sot.data(), (size_t)B * 4, hipMemcpyHostToDevice, st));
     s = decoder_forward(m, g, g.next_tok, 1, nullptr, 0, 0, st);
     if (s != WQ4_OK) return s;
     WA_HIP(wa::launch_argmax(g.logits, B, c.n_vocab, 50259, 50259 + c.n_lang, 0, nullptr, g.prompt_tok, 3,
@@ -1116,65 +1108,16 @@ wq4_status prompt_body(wa_model* m, DecGroup& g, bool explicit_lang, hipStream_t
     // position counter continues at 1 + 3 = 4 (whisper.rs:74,93).
     s = decoder_forward(m, g, g.prompt_tok, 3, nullptr, 0, 0, st);
     if (s != WQ4_OK) return s;
+    pos0 = 4;
+    kv0 = 3;
   }
   // first token: EOT suppressed (whisper.rs:97-99)
   WA_HIP(wa::launch_argmax(g.logits, B, c.n_vocab, 0, c.n_vocab, 1, nullptr, g.next_tok, 1, m->range_flag, st));
-  WA_HIP(hipMemcpyAsync(g.state, g.state_init + (explicit_lang ? 0 : 1), sizeof(wa::DecodeState),
-                        hipMemcpyDeviceToDevice, st));
+  const wa::DecodeState init{pos0 - 1, kv0 - 1, -1, 0};
+  WA_HIP(hipMemcpyAsync(g.state, &init, sizeof(init), hipMemcpyHostToDevice, st));
   WA_HIP(hipMemsetAsync(g.ntok, 0, (size_t)B * 4, st));
   WA_HIP(hipMemsetAsync(g.done, 0, (size_t)B * 4, st));
   WA_HIP(hipMemsetAsync(g.tokens, 0, (size_t)B * kMaxTokens * 4, st));
-  return WQ4_OK;
-}
-
-wq4_status prompt_group(wa_model* m, DecGroup& g, int lang_token, hipStream_t st) {
-  const Config& c = m->cfg;
-  const int B = g.nb;
-  const bool explicit_lang = lang_token >= 0;
-  // the prompt tokens: uploaded (synchronously) when the language or the
-  // clip count changes -- every earlier transcribe has run its prompt by
-  // then (wa_transcribe and wa_transcribe_batches return after their
-  // decodes), so no queued prompt still reads the old tokens
-  if (g.prompt_lang != lang_token || g.prompt_nb != B) {
-    std::vector<int> ptok((size_t)B * 4);
-    for (int b = 0; b < B; ++b) {
-      if (explicit_lang) {
-        ptok[b * 4 + 0] = kSOT;
-        ptok[b * 4 + 1] = lang_token;
-        ptok[b * 4 + 2] = c.transcribe_token();
-        ptok[b * 4 + 3] = c.no_timestamps_token();
-      } else {  // [lang (written by the language pick), TRANSCRIBE, NO_TIMESTAMPS]
-        ptok[b * 3 + 0] = kSOT;
-        ptok[b * 3 + 1] = c.transcribe_token();
-        ptok[b * 3 + 2] = c.no_timestamps_token();
-      }
-    }
-    WA_HIP(hipMemcpy(g.prompt_init, ptok.data(), (size_t)B * 4 * 4, hipMemcpyHostToDevice));
-    g.prompt_lang = lang_token;
-    g.prompt_nb = B;
-  }
-  // everything the captured prompt bakes in: the clip range, the prompt
-  // form, the cross-attention form and the range tier
-  const int64_t key = ((((int64_t)g.b0 * 512 + g.nb) * 2 + (explicit_lang ? 1 : 0)) * 2 + (m->group_kv(g) ? 1 : 0)) * 3 +
-                      (m->wide_ffn ? 2 : m->wide_range ? 1 : 0);
-  if (!(g.pgraph && g.pgraph_key == key)) {
-    if (g.pgraph) {
-      (void)hipGraphExecDestroy(g.pgraph);
-      g.pgraph = nullptr;
-    }
-    WA_WQ4(wq4_prepare_stream(m->device, st));  // split-K workspace exists before capture
-    hipGraph_t gr;
-    WA_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-    wq4_status s = prompt_body(m, g, explicit_lang, st);
-    hipError_t ce = hipStreamEndCapture(st, &gr);
-    if (s != WQ4_OK) return s;
-    if (ce != hipSuccess) return fail(WQ4_EHIP, std::string("prompt graph capture: ") + hipGetErrorString(ce));
-    ce = hipGraphInstantiate(&g.pgraph, gr, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(gr);
-    if (ce != hipSuccess) return fail(WQ4_EHIP, std::string("prompt graph instantiate: ") + hipGetErrorString(ce));
-    g.pgraph_key = key;
-  }
-  WA_HIP(hipGraphLaunch(g.pgraph, st));
   return WQ4_OK;
 }
 
