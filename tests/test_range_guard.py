@@ -209,3 +209,28 @@ def test_normal_model_never_flags():
     m.transcribe(mel, None, STEPS, eot_stop=True)
     assert not m.wide_range and m.range_tier == 0
     m.close()
+
+
+@pytest.mark.gpu
+def test_pipelined_batches_recover_through_the_tiers(tmp_path):
+    """wa_transcribe_batches on the fc1 stress model: the first batch flags in
+    the pipeline, is re-run through wa_transcribe's tiers (tier 2), and every
+    batch -- including those decoded after the model went to tier 2 -- gives
+    the f32 oracle's tokens; a value overflow still fails loudly."""
+    import torch
+
+    import whisper_amd
+    import wq4
+
+    t32, _, _, _, _ = oracle_run("fc1")
+    m = whisper_amd.WhisperModel.from_gguf(_write("fc1", tmp_path), "tiny_test", max_batch=len(CLIPS))
+    mel = torch.from_numpy(_mels(m.config["n_mels"])).cuda()
+    out = m.transcribe_batches(torch.stack([mel, mel, mel]), 50259, STEPS, eot_stop=False)
+    assert m.range_tier == 2
+    assert out == [t32, t32, t32]
+    m.close()
+    m = whisper_amd.WhisperModel.from_gguf(_write("value", tmp_path), "tiny_test", max_batch=len(CLIPS))
+    with pytest.raises(wq4.WQ4Error) as ei:
+        m.transcribe_batches(torch.stack([mel, mel]), 50259, STEPS, eot_stop=False)
+    assert ei.value.status == 7
+    m.close()
