@@ -1307,16 +1307,6 @@ __global__ void bookkeep_kernel(const int* __restrict__ next, int* __restrict__ 
   }
 }
 
-// A/B probe: one workgroup that waits `us` microseconds (100 MHz real-time clock).
-__global__ void delay_kernel(long long ticks) {
-  const long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
-}
-hipError_t launch_delay(int us, hipStream_t st) {
-  hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, st, (long long)us * 100);
-  return hipGetLastError();
-}
-
 hipError_t launch_bookkeep(const int* next_tok, int* tokens, int* n_tokens, int* done, int B, int max_tokens,
                            int eot_stop, DecodeState* state, hipStream_t st) {
   hipLaunchKernelGGL(bookkeep_kernel, dim3(1), dim3(256), 0, st, next_tok, tokens, n_tokens, done, B, max_tokens,

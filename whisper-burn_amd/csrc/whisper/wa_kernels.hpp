@@ -132,7 +132,6 @@ hipError_t launch_emb_tiled(const float* emb, int V, int D, int ns, _Float16* ou
 // Greedy-loop bookkeeping at the top of each step (whisper.rs:104-115):
 // for every clip not yet done, EOT -> done (eot_stop != 0), else append the
 // next token; then advance position / kv_len / step.
-hipError_t launch_delay(int us, hipStream_t st);
 hipError_t launch_bookkeep(const int* next_tok, int* tokens, int* n_tokens, int* done, int B, int max_tokens,
                            int eot_stop, DecodeState* state, hipStream_t st);
 

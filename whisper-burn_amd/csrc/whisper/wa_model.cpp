@@ -1428,8 +1428,6 @@ wq4_status run_decode(wa_model* m, int B, int lang_token, int max_tokens, int eo
     s = ensure_graph(m, g, eot_stop);
     if (s != WQ4_OK) return s;
   }
-  if (const char* e = getenv("WA_GROUP_SKEW_US"); e && G > 1)  // A/B probe: phase offset of group 1
-    WA_HIP(wa::launch_delay(atoi(e), m->groups[1].st));
   // greedy loop (whisper.rs:104-125): each step replays every live group's
   // graph; a group stops once all its clips emitted EOT (polled with a lag)
   EventSet ev;
