@@ -28,7 +28,26 @@ MODES = [int(v) for v in os.environ.get("MODES", "0,2,3").split(",")]
 SHAPES = [(3840, 1280), (1280, 1280), (5120, 1280), (1280, 5120)]
 
 
+def masked_stream(n):
+    """MASK_CUS=n: a stream on CU-mask bits 0..n-1 (n / 8 CUs of every XCD),
+    the pipelined transcribe's encoder stream."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    words = (ctypes.c_uint32 * 8)()
+    for i in range(n):
+        words[i // 32] |= 1 << (i % 32)
+    s = ctypes.c_void_p()
+    assert hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(8), words) == 0
+    return torch.cuda.ExternalStream(s.value)
+
+
 def main():
+    if os.environ.get("MASK_CUS"):
+        with torch.cuda.stream(masked_stream(int(os.environ["MASK_CUS"]))):
+            return run_all()
+    return run_all()
+
+
+def run_all():
     L = wq4.lib()
     vp = ctypes.c_void_p
     st = vp(torch.cuda.current_stream().cuda_stream)
