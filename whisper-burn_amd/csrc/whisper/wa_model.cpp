@@ -1591,9 +1591,12 @@ wq4_status transcribe_pipelined(wa_model* m, const float* mel_dev, int NB, int B
   int32_t* host = nullptr;
   const size_t per = (size_t)B * kMaxTokens + B + 1;
   WA_HIP(hipHostMalloc(reinterpret_cast<void**>(&host), (size_t)NB * per * 4, 0));
-  struct HostGuard {
+  struct HostGuard {  // an early error return may leave copies into `p` queued: drain them first
     int32_t* p;
-    ~HostGuard() { (void)hipHostFree(p); }
+    ~HostGuard() {
+      (void)hipDeviceSynchronize();
+      (void)hipHostFree(p);
+    }
   } hg{host};
   EventSet ev;
   struct Batch {
