@@ -41,6 +41,31 @@ __device__ __forceinline__ float epi_value_pre(float acc, float bias, float res,
   return v;
 }
 
+// f32 epilogue of one 32 x 32 accumulator tile (this lane: column col,
+// element i at row row_of(i), stored at out[idx(row, col)]): the bias and
+// all 16 residuals are loaded before the first store.  Element by element
+// (epi_value) the compiler cannot move a residual load above the previous
+// element's store -- y may alias residual (in-place residual adds) -- so the
+// tile paid 16 dependent memory round trips; this way it pays one.  Same
+// arithmetic as epi_value: the same bits.
+template <class RowOf, class Idx>
+__device__ __forceinline__ void epi_store_tile(const floatx16& acc, float cs, int col, RowOf row_of, Idx idx,
+                                               const EpiArgs& e) {
+  const bool cok = col < e.n;
+  const float b = (e.bias && cok) ? e.bias[col] : 0.0f;
+  float res[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = row_of(i);
+    res[i] = (e.residual && cok && row < e.m) ? e.residual[(size_t)row * e.ldo + col] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = row_of(i);
+    if (cok && row < e.m) e.out[idx(row, col)] = epi_value_pre(acc[i] * cs, b, res[i], e);
+  }
+}
+
 // One repacked u32 (8 nibbles, see wq4_layout.hpp) -> 8 exact f16 (q - 8),
 // element order j = 0..7:
 //   (w & 0x000F000F) | 0x64006400 = f16 pair (1024 + q_a, 1024 + q_b)

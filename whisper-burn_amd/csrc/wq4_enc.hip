@@ -306,14 +306,12 @@ __global__ __launch_bounds__(64 * WM * 4, WM == 2 ? 2 : 3) void q4_gemm_enc_kern
     for (int mt = 0; mt < TM; ++mt)
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int row = (mt0 + mt) * 32 + acc_row_e(i, h);
-          const int col = (nt0 + nt) * 32 + r;
-          if (row < e.m && col < e.n)
-            e.out[EPI == kEpiHeadMajor ? out_index(e, row, col) : (size_t)row * e.ldo + col] =
-                epi_value(acc[mt][nt][i] * cs[nt], row, col, e);
-        }
+        epi_store_tile(
+            acc[mt][nt], cs[nt], (nt0 + nt) * 32 + r, [&](int i) { return (mt0 + mt) * 32 + acc_row_e(i, h); },
+            [&](int row, int col) {
+              return EPI == kEpiHeadMajor ? out_index(e, row, col) : (size_t)row * e.ldo + col;
+            },
+            e);
   } else {
     static_assert(EPI == kEpiTiled, "f32, head-major f32 or A-tiled outputs");
     float* stage = reinterpret_cast<float*>(smem) + wave * (32 * kStageLdE);

@@ -345,13 +345,9 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
       for (int mt = 0; mt < TM; ++mt)
 #pragma unroll
         for (int nt = 0; nt < TN; ++nt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int row = (TM * mg + mt) * 32 + acc_row(i, h);
-            const int col = (nt0 + nt) * 32 + r;
-            if (row < e.m && col < e.n)
-              e.out[(size_t)row * e.ldo + col] = epi_value(acc[mt][nt][i] * cs[nt], row, col, e);
-          }
+          epi_store_tile(
+              acc[mt][nt], cs[nt], (nt0 + nt) * 32 + r, [&](int i) { return (TM * mg + mt) * 32 + acc_row(i, h); },
+              [&](int row, int col) { return (size_t)row * e.ldo + col; }, e);
     }
   } else if constexpr (EPI == kEpiHeadMajor) {
     if (active) {
@@ -451,13 +447,9 @@ __device__ __forceinline__ void decode_epilogue(const floatx16& s, float cs, int
   const int r = lane & 31, h = lane >> 5;
   const int col = nt * 32 + r;
   if constexpr (EPI != kEpiTiled) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = mt * 32 + acc_row(i, h);
-      if (row < e.m && col < e.n)
-        e.out[EPI == kEpiHeadMajor ? out_index(e, row, col) : (size_t)row * e.ldo + col] =
-            epi_value(s[i] * cs, row, col, e);
-    }
+    epi_store_tile(
+        s, cs, col, [&](int i) { return mt * 32 + acc_row(i, h); },
+        [&](int row, int c) { return EPI == kEpiHeadMajor ? out_index(e, row, c) : (size_t)row * e.ldo + c; }, e);
   } else {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
