@@ -396,10 +396,13 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
             const float v = (row < e.m && col < e.n) ? epi_value(acc[mt][nt][i] * cs[nt], row, col, e) : 0.0f;
             stage[rl * kStageLd + nt * 32 + r] = v;
           }
+        // the stage is this wave's own (the K loop's last barrier freed the
+        // A buffers under it): a wave-local hand-off, no workgroup barrier
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): stage writes visible to this wave
+        __builtin_amdgcn_wave_barrier();
+        store_tiled_slab<NS, TN>(stage, e, TM * mg + mt, nt0, lane);
+        __builtin_amdgcn_wave_barrier();
       }
-      __syncthreads();
-      if (active) store_tiled_slab<NS, TN>(stage, e, TM * mg + mt, nt0, lane);
-      __syncthreads();
     }
   }
 }
