@@ -62,10 +62,13 @@ constexpr int kMinTokens = 3;    // whisper.rs:97
 // Pipelined transcribes (transcribe_pipelined): CUs of the encoder stream
 // that runs beside a decode, the encoder layers it covers in the first
 // overlapped batch, and the share of the last decode's length its part is
-// sized to afterwards (WA_ENC_CUS / WA_ENC_OVERLAP override).
+// sized to afterwards (WA_ENC_CUS / WA_ENC_OVERLAP / WA_ENC_FILL override).
+// Fill measured at 32 clips (scripts/r05ad.sh): RTF 959 at 0.92, 966 at 0.98
+// / 1.0 / 1.02, 948 at 1.04 (the masked part then outlasts the decode);
+// 0.98 keeps ~30 ms of slack.
 constexpr int kEncOverlapCUs = 32;
 constexpr int kEncOverlapLayers0 = 16;
-constexpr double kEncOverlapFill = 0.92;
+constexpr double kEncOverlapFill = 0.98;
 
 struct Config {  // WhisperConfig, src/model/config.rs:5-30
   int n_mels, n_audio_ctx, n_audio_state, n_audio_head, n_audio_layer;
@@ -1644,7 +1647,9 @@ wq4_status transcribe_pipelined(wa_model* m, const float* mel_dev, int NB, int B
       WA_HIP(hipEventElapsedTime(&tm, p.mstart, p.mend));
       if (!getenv("WA_ENC_OVERLAP")) {
         const double per_layer = tm / (double)(p.k + 1);  // the conv stem counts as one layer
-        m->overlap_k = std::max(0, std::min(L, (int)(kEncOverlapFill * td / per_layer) - 1));
+        double fill = kEncOverlapFill;
+        if (const char* e = getenv("WA_ENC_FILL")) fill = atof(e);  // A/B only
+        m->overlap_k = std::max(0, std::min(L, (int)(fill * td / per_layer) - 1));
       }
     }
     if (const char* e = getenv("WA_ENC_OVERLAP")) m->overlap_k = std::max(0, std::min(L, atoi(e)));
