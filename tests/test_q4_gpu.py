@@ -351,6 +351,58 @@ def test_linear_ws_residual_and_gelu(torch):
     assert np.max(np.abs(y.cpu().numpy() - want)) < 1e-4
 
 
+def _identity_q4(n):
+    """Q4_0 bytes of the n x n identity: d = 1, nibble 9 (q = 1) on the diagonal."""
+    nb = n // 32
+    raw = bytearray()
+    for r in range(n):
+        for b in range(nb):
+            q = [8] * 32
+            if r // 32 == b:
+                q[r % 32] = 9
+            raw += np.float16(1.0).tobytes() + bytes((q[i] | (q[i + 16] << 4)) for i in range(16))
+    return np.frombuffer(bytes(raw), np.uint8)
+
+
+@pytest.mark.parametrize("m", [16, 3000])
+def test_gelu_epilogue_vs_float64(torch, m):
+    """The GEMM epilogue's GELU (evaluated as x / (1 + 2^t), wq4_device.hpp)
+    against float64 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
+    (layers.rs:35-41) through an exact identity weight: relative error a few
+    f32 ulps over x in [-12, 12], including the negative tail where the f32
+    tanh form cancels (decode-size and encoder-size row counts)."""
+    import ctypes
+
+    n = 64
+    t = wq4.Q4Tensor.from_q4_bytes(_identity_q4(n), [n, n])
+    rng = np.random.default_rng(5)
+    x = np.concatenate([np.linspace(-12.0, 12.0, m * n // 2), rng.standard_normal(m * n - m * n // 2) * 3.0])
+    x = x.astype(np.float32)
+    xd = to_dev(torch, x, (m, n))
+    b = torch.zeros(n, device="cuda:0")
+    y = torch.zeros((m, n), device="cuda:0")
+    nbytes = wq4.lib().wq4_linear_workspace_bytes(t.handle, m)
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device="cuda:0")
+    vp = ctypes.c_void_p
+    wq4.check(wq4.lib().wq4_linear_forward_ws(t.handle, vp(b.data_ptr()), vp(xd.data_ptr()), None,
+                                              vp(y.data_ptr()), m, n, wq4.EPI_GELU, wq4.PREC_F16X2,
+                                              vp(ws.data_ptr()), nbytes,
+                                              vp(torch.cuda.current_stream().cuda_stream)))
+    x64 = x.astype(np.float64)
+    u = 0.7978845608028654 * (x64 + 0.044715 * x64**3)
+    # 0.5 x (1 + tanh u) == x / (1 + e^(-2u)); the latter has no cancellation
+    # in float64 either where tanh u -> -1
+    want = x64 / (1.0 + np.exp(-2.0 * u))
+    tanh_form = 0.5 * x64 * (1.0 + np.tanh(u))
+    ok = np.abs(want) > 1e-6
+    assert np.allclose(want[ok], tanh_form[ok], rtol=1e-9, atol=0)
+    got = y.cpu().numpy().reshape(-1).astype(np.float64)
+    # the operand split holds x to 2^-22 relative; GELU's slope is <= 1.13
+    err = np.abs(got - want)
+    bound = 2e-6 * np.abs(x64) + 1e-6 * np.abs(want) + 1e-37
+    assert np.all(err <= bound), float(np.max(err / bound))
+
+
 @pytest.mark.parametrize("policy", [1, 2])
 def test_gemm_headmajor_layout(torch, policy):
     """wq4_gemm_tiled_headmajor == row-major GEMM permuted to [part][g][head][t][64]."""
