@@ -397,9 +397,13 @@ def test_gelu_epilogue_vs_float64(torch, m):
     ok = np.abs(want) > 1e-6
     assert np.allclose(want[ok], tanh_form[ok], rtol=1e-9, atol=0)
     got = y.cpu().numpy().reshape(-1).astype(np.float64)
-    # the operand split holds x to 2^-22 relative; GELU's slope is <= 1.13
+    # the operand split holds x to 2^-22 relative (GELU's slope is <= 1.13),
+    # except below |x| = 2^-7: with the 2^4 operand scale the lo half is then
+    # an f16 subnormal, which the MFMA flushes -- x to
+    # 2^-11 relative there, times GELU's slope ~1/2 near 0
     err = np.abs(got - want)
-    bound = 2e-6 * np.abs(x64) + 1e-6 * np.abs(want) + 1e-37
+    ax = np.abs(x64)
+    bound = 2e-6 * ax + 1e-6 * np.abs(want) + np.where(ax < 2.0**-7, 2.0**-12 * ax, 0.0) + 1e-37
     assert np.all(err <= bound), float(np.max(err / bound))
 
 
