@@ -440,12 +440,12 @@ def test_gemm_headmajor_layout(torch, policy):
                                              ctypes.c_void_p(hm.data_ptr()), m, 25, d, wq4.PREC_F16X2, policy, st))
 
 
-@pytest.mark.parametrize("clips", [1, 2])
-def test_gemm_headmajor_ring_kernel(torch, clips):
+@pytest.mark.parametrize("clips,mode", [(1, 1), (2, 1), (2, 5), (9, 5)])
+def test_gemm_headmajor_ring_kernel(torch, clips, mode):
     """The few-clip cross K / V cache GEMMs (wa_model.cpp cross_kv_forward:
     M = clips x 1500 rows, head-major output) run on the encoder ring kernel
-    (wq4_enc.hip); their bits equal the prefill tile kernel's row-major
-    result permuted to [g][head][t][64]."""
+    (wq4_enc.hip; mode 5: the wide kernel, wq4_wide.hip); their bits equal
+    the prefill tile kernel's row-major result permuted to [g][head][t][64]."""
     import ctypes
 
     d = k = 1280
@@ -467,7 +467,7 @@ def test_gemm_headmajor_ring_kernel(torch, clips):
     try:
         wq4.check(L.wq4_gemm_tiled(t.handle, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(at.data_ptr()), None,
                                    ctypes.c_void_p(ref.data_ptr()), None, m, 0, wq4.PREC_F16X2, 1, st))
-        assert L.wq4_debug_set_enc_kernel(1) >= 0  # by rows: the ring kernel at these grids
+        assert L.wq4_debug_set_enc_kernel(mode) >= 0  # 1: by rows (the ring kernel at these grids)
         wq4.check(L.wq4_gemm_tiled_headmajor(t.handle, ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(at.data_ptr()),
                                              ctypes.c_void_p(hm.data_ptr()), m, trows, d, wq4.PREC_F16X2, 0, st))
         torch.cuda.synchronize()
@@ -792,16 +792,19 @@ def test_f16_weights_out_of_decode_step_range(torch):
 
 
 # ------------------------------- encoder GEMM: LDS-DMA ring kernel (wq4_enc.hip) --
-@pytest.mark.parametrize("m,n,k,flags", [(1500, 1280, 1280, 0), (3000, 3840, 1280, 0), (700, 5120, 1280, 5),
-                                         (300, 1280, 5120, 2), (2049, 1280, 1280, 1), (16000, 1280, 1280, 2),
-                                         (4500, 5120, 1280, 5), (200, 96, 160, 0), (1000, 1312, 1280, 4)])
-def test_enc_kernel_bit_identical(torch, m, n, k, flags):
-    """The encoder-size GEMM ring kernel (its geometries: 256 x 256 with 8
-    waves, 64 x 128 and 32 x 256 with 4) gives the prefill tile kernel's bits
-    exactly: the same
-    per-block MFMA chain and scale FMA order, only the memory pipeline
-    differs.  flags: 1 GELU, 2 residual, 4 A-tiled output (then compared
-    fragment for fragment, padding included)."""
+@pytest.mark.parametrize("m,n,k,flags,prec", [(1500, 1280, 1280, 0, 0), (3000, 3840, 1280, 0, 0), (700, 5120, 1280, 5, 0),
+                                              (300, 1280, 5120, 2, 0), (2049, 1280, 1280, 1, 0), (16000, 1280, 1280, 2, 0),
+                                              (4500, 5120, 1280, 5, 0), (200, 96, 160, 0, 0), (1000, 1312, 1280, 4, 0),
+                                              (2049, 1280, 1280, 4, 0), (1500, 1280, 5120, 3, 0), (2000, 5120, 1280, 5, 1),
+                                              (300, 1312, 160, 4, 1)])
+def test_enc_kernel_bit_identical(torch, m, n, k, flags, prec):
+    """The encoder-size GEMM kernels -- the ring kernel (its geometries: 256 x
+    256 with 8 waves, 64 x 128 and 32 x 256 with 4) and the 8-wave wide
+    kernel (wq4_wide.hip, mode 5) -- give the prefill tile kernel's bits
+    exactly: the same per-block MFMA chain and scale FMA order, only the
+    memory pipeline differs.  flags: 1 GELU, 2 residual, 4 A-tiled output
+    (then compared fragment for fragment, padding included).  prec 1 (f16
+    operands): the ring kernel is f16x2-only, so the tile and wide kernels."""
     import ctypes
 
     rng = np.random.default_rng(m + n + k + flags)
@@ -811,26 +814,27 @@ def test_enc_kernel_bit_identical(torch, m, n, k, flags):
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     p = lambda a: ctypes.c_void_p(a.data_ptr()) if a is not None else None  # noqa: E731
     x = to_dev(torch, rng.standard_normal(m * k).astype(np.float32), (m, k))
-    at = torch.zeros(L.wq4_atiled_bytes(m, k, 0), dtype=torch.uint8, device="cuda:0")
-    wq4.check(L.wq4_tile_activations(p(x), m, k, k, 0, p(at), at.numel(), st))
+    at = torch.zeros(L.wq4_atiled_bytes(m, k, prec), dtype=torch.uint8, device="cuda:0")
+    wq4.check(L.wq4_tile_activations(p(x), m, k, k, prec, p(at), at.numel(), st))
     b = to_dev(torch, (rng.standard_normal(n) * 0.1).astype(np.float32), (n,))
     res = to_dev(torch, rng.standard_normal(m * n).astype(np.float32), (m, n))
     tiled = (flags & 4) != 0
+    modes = (0, 2, 3, 4, 5, 1) if prec == 0 else (0, 5, 1)
     outs = []
     prev = L.wq4_debug_set_enc_kernel(0)
     try:
-        for mode in (0, 2, 3, 4, 1):
+        for mode in modes:
             assert L.wq4_debug_set_enc_kernel(mode) >= 0
             y = res.clone() if flags & 2 else torch.full((m, n), 7.0, device="cuda:0")
-            ot = torch.full((L.wq4_atiled_bytes(m, n, 0),), 0x5A, dtype=torch.uint8, device="cuda:0") if tiled else None
+            ot = torch.full((L.wq4_atiled_bytes(m, n, prec),), 0x5A, dtype=torch.uint8, device="cuda:0") if tiled else None
             wq4.check(L.wq4_gemm_tiled(t.handle, p(b), p(at), p(y) if flags & 2 else None, None if tiled else p(y),
-                                       p(ot), m, flags, 0, 1, st))
+                                       p(ot), m, flags, prec, 1, st))
             torch.cuda.synchronize()
             outs.append((ot if tiled else y).cpu().numpy().copy())
     finally:
         L.wq4_debug_set_enc_kernel(prev)
     ref = outs[0]
-    for mode, o in zip((2, 3, 4, 1), outs[1:]):
+    for mode, o in zip(modes[1:], outs[1:]):
         if tiled:
             assert np.array_equal(o, ref), f"A-tiled output differs in mode {mode}"
         else:

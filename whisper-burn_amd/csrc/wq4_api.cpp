@@ -266,9 +266,11 @@ const char* wq4_gemm_kernel_name(int64_t n, int64_t k, int64_t rows) {
     case 3: return "skinny_gemm_kernel";
     case 2: return "q4_gemm_decode_kernel";
     default:
-      return wq4::enc_gemm_pick(g, (int)rows, 0, g_prec.load() == WQ4_PREC_F16X2 ? 2 : 1, 0) != 0
-                 ? "q4_gemm_enc_kernel"
-                 : "q4_gemm_prefill_kernel";
+      switch (wq4::enc_gemm_pick(g, (int)rows, 0, g_prec.load() == WQ4_PREC_F16X2 ? 2 : 1, 0)) {
+        case 0: return "q4_gemm_prefill_kernel";
+        case 5: return "q4_gemm_wide_kernel";
+        default: return "q4_gemm_enc_kernel";
+      }
   }
 }
 

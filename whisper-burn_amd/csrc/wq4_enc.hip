@@ -368,7 +368,7 @@ __global__ __launch_bounds__(64 * WM * 4, WM == 2 ? 2 : 3) void q4_gemm_enc_kern
 // Launcher.
 // ------------------------------------------------------------------------
 // 0 = off (the prefill tile kernel), 1 = by rows (enc_gemm_pick), 2 = always
-// L, 3 = always S.
+// L, 3 = always S, 5 = always the wide kernel (wq4_wide.hip).
 // Initialised from WQ4_ENC_KERNEL (default 1); wq4_debug_set_enc_kernel
 // switches it at run time (A/B and bit-equality tests in one process).
 static std::atomic<int> g_enc_mode{[] {
@@ -388,9 +388,9 @@ static std::atomic<int> g_enc_mode{[] {
 // < 400 workgroups, the tile kernel above.
 int enc_gemm_pick(const Q4Geom& g, int rows, int epi_mode, int ns, int wtype) {
   const int mode = g_enc_mode.load();
-  if (mode == 0 || ns != 2 || wtype != kWeightsQ4 || rows <= 128 ||
-      g.kb < 1)
-    return 0;
+  if (mode == 0 || wtype != kWeightsQ4 || rows <= 128 || g.kb < 1) return 0;
+  if (mode == 5) return wide_gemm_supported(g, rows, ns, wtype) ? 5 : 0;
+  if (ns != 2) return 0;  // the ring kernel: f16x2 operands only
   if (mode >= 2) return mode;
   const int64_t mt = round_up(rows, kMPad) / kMTile;
   const int64_t tile_grid = ((mt + 3) / 4) * ((g.ntiles + 7) / 8);
@@ -428,7 +428,7 @@ hipError_t launch_enc_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* 
 }  // namespace wq4
 
 extern "C" int wq4_debug_set_enc_kernel(int mode) {
-  if (mode < 0 || mode > 4) return -1;
+  if (mode < 0 || mode > 5) return -1;
   const int prev = wq4::g_enc_mode.load();
   wq4::g_enc_mode.store(mode);
   return prev;

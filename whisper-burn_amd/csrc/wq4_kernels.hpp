@@ -60,10 +60,16 @@ hipError_t launch_q4_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* s
 // The encoder-size GEMM ring kernel (wq4_enc.hip): Q4_0 weights, f16x2
 // operands, f32 or A-tiled outputs, rows > 128 -- bit-identical to the
 // prefill tile kernel's results.  enc_gemm_pick: 0 = use the tile kernel,
-// else the geometry (2 = L, 3 = S) to pass to launch_enc_gemm.
+// else the geometry (2 = L, 3 = S) to pass to launch_enc_gemm, or 5 = the
+// wide kernel (launch_wide_gemm).
 int enc_gemm_pick(const Q4Geom& g, int rows, int epi_mode, int ns, int wtype);
 hipError_t launch_enc_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* cs,
                            const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int geo, hipStream_t st);
+// The 8-wave wide kernel (wq4_wide.hip, enc_gemm_pick geometry 5): Q4_0
+// weights, rows > 128, NS = 1 or 2 -- bit-identical to the tile kernel.
+bool wide_gemm_supported(const Q4Geom& g, int rows, int ns, int wtype);
+hipError_t launch_wide_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* cs,
+                            const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int ns, hipStream_t st);
 
 // The decode-step GEMM (wq4_skinny.hip): rows <= 32, 16-column workgroups on
 // 16x16x32 MFMAs, one Q4 block per MFMA with the scale applied per block in

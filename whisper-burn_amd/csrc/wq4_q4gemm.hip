@@ -35,6 +35,7 @@
 #include "wq4_device.hpp"
 #include "wq4_kernels.hpp"
 #include "wq4_lnmath.hpp"
+#include "wq4_tile_epi.hpp"
 
 namespace wq4 {
 
@@ -100,48 +101,6 @@ __global__ __launch_bounds__(256) void tile_activations_kernel(const float* __re
 }
 
 // ------------------------------------------------------------------------
-// Epilogue helpers.
-// ------------------------------------------------------------------------
-constexpr int kStageLd = 68;  // padded f32 row stride of the transpose stage
-
-// Writes one wave's 32-row slab (TN n-tiles of 32 cols) held in `stage`
-// ([32][kStageLd] f32, already epilogue-applied) as A-tiled f16 fragments.
-template <int NS, int TN>
-__device__ __forceinline__ void store_tiled_slab(const float* stage, const EpiArgs& e, int mt_g, int nt_g0,
-                                                 int lane) {
-  const int r = lane & 31, h = lane >> 5;
-  half8* dst = reinterpret_cast<half8*>(e.out_tiled);
-  const size_t kbp_next = (size_t)e.nbp_next * 2;
-#pragma unroll
-  for (int nt = 0; nt < TN; ++nt) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const float* src = stage + r * kStageLd + nt * 32 + kk * 16 + h * 8;
-      const floatx4 a = *reinterpret_cast<const floatx4*>(src);
-      const floatx4 c = *reinterpret_cast<const floatx4*>(src + 4);
-      half8 hi, lo;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        _Float16 x, y;
-        split_act(a[j], x, y);
-        hi[j] = x;
-        lo[j] = y;
-        split_act(c[j], x, y);
-        hi[4 + j] = x;
-        lo[4 + j] = y;
-      }
-      const size_t frag = (((size_t)mt_g * kbp_next + (nt_g0 + nt)) * 2 + kk) * NS;
-      dst[(frag + 0) * 64 + lane] = hi;
-      if constexpr (NS == 2) dst[(frag + 1) * 64 + lane] = lo;
-    }
-  }
-}
-
-// acc[i] of a 32x32 tile: row (i&3) + 8*(i>>2) + 4*h, column r (C/D layout of
-// v_mfma_f32_32x32x16_*, cdna_hip_programming.md §3).
-__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
-
-// ------------------------------------------------------------------------
 // Prefill / encoder kernel.
 // ------------------------------------------------------------------------
 constexpr int kPrefillTM = 4;  // m-tiles (32 rows) per workgroup
@@ -162,7 +121,7 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
   constexpr int SEGS_PER_CHUNK = CHUNK / 1024;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
+  const int r = lane & 31;
   const int ngroups = (ntiles + 4 * TN - 1) / (4 * TN);
   const int mgroups = mtiles / TM;
   const int wg = xcd_remap(blockIdx.x, ngroups * mgroups);
@@ -334,77 +293,8 @@ __global__ __launch_bounds__(256, 2) void q4_gemm_prefill_kernel(const uint8_t* 
     __syncthreads();  // drains this step's global_load_lds before the next read
   }
 
-  float cs[TN];
-  const float ainv = e.act_inv ? *e.act_inv : kActScaleInv;  // A operand scale (exact power of two)
-#pragma unroll
-  for (int nt = 0; nt < TN; ++nt) cs[nt] = active ? colscale[(nt0 + nt) * 32 + r] * ainv : 1.0f;
-
-  if constexpr (EPI == kEpiF32) {
-    if (active) {
-#pragma unroll
-      for (int mt = 0; mt < TM; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < TN; ++nt)
-          epi_store_tile(
-              acc[mt][nt], cs[nt], (nt0 + nt) * 32 + r, [&](int i) { return (TM * mg + mt) * 32 + acc_row(i, h); },
-              [&](int row, int col) { return (size_t)row * e.ldo + col; }, e);
-    }
-  } else if constexpr (EPI == kEpiHeadMajor) {
-    if (active) {
-      // one division per m-tile and n-tile, not per element (out_index)
-      size_t cofs[TN];
-#pragma unroll
-      for (int nt = 0; nt < TN; ++nt) {
-        const int col = (nt0 + nt) * 32 + r;
-        const int part = col / e.hm_d, c = col - part * e.hm_d;
-        cofs[nt] = (size_t)part * e.m * e.hm_d + (size_t)(c >> 6) * e.hm_t * 64 + (c & 63);
-      }
-      const size_t gstride = (size_t)(e.hm_d >> 6) * e.hm_t * 64;
-#pragma unroll
-      for (int mt = 0; mt < TM; ++mt) {
-        const int r0 = (TM * mg + mt) * 32;
-        const int g0 = r0 / e.hm_t, t0 = r0 - g0 * e.hm_t;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int rl = acc_row(i, h), row = r0 + rl;
-          int t = t0 + rl, g = g0;
-          while (t >= e.hm_t) {  // at most one step when hm_t >= 32
-            t -= e.hm_t;
-            ++g;
-          }
-          const size_t rofs = (size_t)g * gstride + (size_t)t * 64;
-#pragma unroll
-          for (int nt = 0; nt < TN; ++nt) {
-            const int col = (nt0 + nt) * 32 + r;
-            if (row < e.m && col < e.n) e.out[rofs + cofs[nt]] = epi_value(acc[mt][nt][i] * cs[nt], row, col, e);
-          }
-        }
-      }
-    }
-  } else {
-    float* stage = reinterpret_cast<float*>(smem) + wave * (32 * kStageLd);
-#pragma unroll
-    for (int mt = 0; mt < TM; ++mt) {
-      if (active) {
-#pragma unroll
-        for (int nt = 0; nt < TN; ++nt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int rl = acc_row(i, h);
-            const int row = (TM * mg + mt) * 32 + rl;
-            const int col = (nt0 + nt) * 32 + r;
-            const float v = (row < e.m && col < e.n) ? epi_value(acc[mt][nt][i] * cs[nt], row, col, e) : 0.0f;
-            stage[rl * kStageLd + nt * 32 + r] = v;
-          }
-        // the stage is this wave's own (the K loop's last barrier freed the
-        // A buffers under it): a wave-local hand-off, no workgroup barrier
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): stage writes visible to this wave
-        __builtin_amdgcn_wave_barrier();
-        store_tiled_slab<NS, TN>(stage, e, TM * mg + mt, nt0, lane);
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-  }
+  tile_epilogue<NS, EPI, TM, TN>(acc, TM * mg, nt0, active, mtiles, colscale,
+                                 reinterpret_cast<float*>(smem) + wave * (32 * kStageLd), lane, e);
 }
 
 // ------------------------------------------------------------------------
@@ -1155,6 +1045,7 @@ static hipError_t launch_gemm_t(const Q4Geom& g, const uint8_t* nib, const uint3
     }
 #undef WQ4_DEC
   } else if (const int geo = enc_gemm_pick(g, rows, EPI, NS, WK)) {
+    if (geo == 5) return launch_wide_gemm(g, nib, sc, cs, at, rows, e, EPI, NS, st);
     return launch_enc_gemm(g, nib, sc, cs, at, rows, e, EPI, geo, st);
   } else {
     const int ngroups = (int)((g.ntiles + 4 * kPrefillTN - 1) / (4 * kPrefillTN));

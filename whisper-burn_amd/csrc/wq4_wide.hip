@@ -1,0 +1,466 @@
+// wq4_wide.hip -- the encoder-size Q4_0 GEMM on one 8-wave workgroup per CU.
+//
+// Same arithmetic as q4_gemm_prefill_kernel (wq4_q4gemm.hip), bit for bit:
+// per Q4 block t = MFMA(x_hi, q - 8) + MFMA(x_lo, q - 8) over its two 16-k
+// halves (f32 accumulation from zero), acc = fma(t, d', acc), blocks in K
+// order, y = epi(acc * 2^-s_n * act_inv) -- the reference's
+// shader.wgsl:72-89 contraction with exact products.  What differs is the
+// pipeline around it:
+//
+//  * 256 x 256 output tile per workgroup, 8 waves as 2 (M) x 4 (N), each
+//    wave 128 x 64 (4 x 2 tiles of 32 x 32): one workgroup per CU, two waves
+//    per SIMD, so one wave's block-scale FMAs and dequantisation issue beside
+//    its partner's MFMAs.
+//  * EVERY operand is staged by LDS-DMA (global_load_lds): the A fragments,
+//    the repacked nibbles and the block scales.  No ordinary global load in
+//    the K loop, so hipcc never drains vmcnt(0) there
+//    (cdna_hip_programming.md §5, "Projection GEMM at M = 256" item 4b).
+//  * The K loop runs in half steps of one Q4 block (32 k) through a ring of
+//    four LDS slots: at the top of half step h each wave waits (counted
+//    vmcnt, never 0 in the loop) for its own copies of slot h, one raw
+//    s_barrier publishes them, then the copies of half step h + 3 are issued
+//    into the slot the barrier just freed -- three half steps stay in flight
+//    across the barrier ("Pipelining across barriers").
+//
+// LDS: slots 0 / 2 hold A (8 m-tiles x 2 NS KiB) + nibbles (8 n-tiles x 1
+// KiB, both blocks of the pair) + scales (8 n-tiles x 128 B, twice); slots
+// 1 / 3 hold A only -- the odd half step's weights are read into registers
+// with the even one's.  148 KiB at NS = 2.
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "wq4_device.hpp"
+#include "wq4_kernels.hpp"
+#include "wq4_tile_epi.hpp"
+
+namespace wq4 {
+
+// WQ4_WIDE_DIAG (timing diagnostics only, `make widediag`; 0 in the
+// product): 1 no block-scale FMAs (the MFMA chains accumulate straight into
+// acc), 2 = 1 + no dequantisation (raw nibble words as the B operand).
+#ifndef WQ4_WIDE_DIAG
+#define WQ4_WIDE_DIAG 0
+#endif
+// WQ4_WIDE_STAMP (timing diagnostics only; 0 in the product): per
+// workgroup, waves 0 and 4 record the s_memtime cycles spent in the K loop's
+// vmcnt waits, barriers, LDS-DMA issue and compute, and the loop's total
+// (wq4_diag_wide_stamps).
+#ifndef WQ4_WIDE_STAMP
+#define WQ4_WIDE_STAMP 0
+#endif
+constexpr int kWideStampWgs = 4096;
+#if WQ4_WIDE_STAMP
+__device__ unsigned long long g_wide_stamps[kWideStampWgs * 2 * 5];
+#endif
+
+// WQ4_WIDE_SCHED: the half step's instruction order (A/B builds): 0 the
+// plain two-temporary loop left to the scheduler, 1 three rotating
+// temporaries, the order pinned by sched_barrier, 2 the same order in asm
+// statements (one MFMA + its scale FMAs each).
+#ifndef WQ4_WIDE_SCHED
+#define WQ4_WIDE_SCHED 2
+#endif
+
+// One MFMA of a block chain, t = A B + (first ? 0 : t); nop: open with
+// s_nop 1 (the B operand may have been written by the VALU just before).
+__device__ __forceinline__ void grp_mfma(floatx16& t, const half8& a, const half8& b, bool first, bool nop) {
+  if (first && nop)
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(t) : "v"(a), "v"(b));
+  else if (first)
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(t) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(t) : "v"(a), "v"(b));
+}
+// The same MFMA followed by four scale FMAs c_i = fma(u_i, d, c_i) of an
+// older tile (u: a temporary whose chain has completed).
+__device__ __forceinline__ void grp_mfma_fma(floatx16& t, const half8& a, const half8& b, bool first, bool nop,
+                                             float& c0, float& c1, float& c2, float& c3, float u0, float u1,
+                                             float u2, float u3, float d) {
+  (void)nop;
+  if (first)
+    asm volatile(
+        "v_mfma_f32_32x32x16_f16 %0, %5, %6, 0\n\t"
+        "v_fma_f32 %1, %7, %11, %1\n\t"
+        "v_fma_f32 %2, %8, %11, %2\n\t"
+        "v_fma_f32 %3, %9, %11, %3\n\t"
+        "v_fma_f32 %4, %10, %11, %4"
+        : "=&v"(t), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
+        : "v"(a), "v"(b), "v"(u0), "v"(u1), "v"(u2), "v"(u3), "v"(d));
+  else
+    asm volatile(
+        "v_mfma_f32_32x32x16_f16 %0, %5, %6, %0\n\t"
+        "v_fma_f32 %1, %7, %11, %1\n\t"
+        "v_fma_f32 %2, %8, %11, %2\n\t"
+        "v_fma_f32 %3, %9, %11, %3\n\t"
+        "v_fma_f32 %4, %10, %11, %4"
+        : "+v"(t), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
+        : "v"(a), "v"(b), "v"(u0), "v"(u1), "v"(u2), "v"(u3), "v"(d));
+}
+
+template <int NS>
+struct WideGeo {
+  static constexpr int FR = 2 * NS;                // A fragments (1 KiB) per m-tile and Q4 block
+  static constexpr int AH = 8 * FR * 1024;          // A bytes of one half step
+  static constexpr int BH = 8 * 1024 + 8 * 256;     // nibbles of 8 n-tiles (one block pair) + 8 scale copies
+  static constexpr int PAIR = 2 * AH + BH;          // slot 2p (A + B) then slot 2p + 1 (A)
+  static constexpr int RING = 2 * PAIR;
+  static constexpr int STAGE = 8 * 32 * kStageLd * 4;  // tiled epilogue stage (reuses the ring)
+  static constexpr int LDS = RING > STAGE ? RING : STAGE;
+  static constexpr int CNT0 = FR + 2, CNT1 = FR;    // LDS-DMA copies per wave: even / odd half step
+};
+
+// 4 B per lane: lane l's dword lands at lds_base + 4 l.  (The sub-dword
+// forms also land one dword per lane, so a 2-byte copy is not packed.)
+__device__ __forceinline__ void glds4(const void* gsrc, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_base, 4, 0, 0);
+}
+
+// s_waitcnt vmcnt(N), the other counters untouched (gfx9 encoding).
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void ring_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of the slot being recycled are done
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int NS, int EPI>
+__global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __restrict__ nib,
+                                                              const uint32_t* __restrict__ sc,
+                                                              const float* __restrict__ colscale,
+                                                              const _Float16* __restrict__ at, int mtiles, int nbp,
+                                                              int ntiles, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  using G = WideGeo<NS>;
+  constexpr int TM = 4, TN = 2, FR = G::FR;
+  constexpr int CHUNK = 4096 * NS;  // A bytes per (m-tile, block pair) in global memory
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int r = lane & 31;
+  const int ngroups = (ntiles + 7) / 8, mgroups = (mtiles + 7) / 8;
+  const int wg = xcd_remap(blockIdx.x, ngroups * mgroups);
+  const int mg = wg / ngroups, ng = wg % ngroups;
+  const int nt0 = ng * 8 + wn * TN;
+  const bool active = nt0 < ntiles;  // wave-uniform (ntiles is even)
+
+  // Loader role: wave w copies m-tile 8 mg + w, the nibbles of n-tile
+  // 8 ng + w and the scales of n-tiles 8 ng + 2 (w & 3) + {0, 1} (waves 4-7
+  // copy those of 0-3 again, so every wave issues the same count); indices
+  // are clamped to the last tile: the duplicate rows / columns are never
+  // stored.
+  const uint8_t* asrc =
+      reinterpret_cast<const uint8_t*>(at) + (size_t)min(mg * 8 + wave, mtiles - 1) * nbp * CHUNK + lane * 16;
+  const int lnt = min(ng * 8 + wave, ntiles - 1);
+  const uint8_t* nsrc = nib + (size_t)lnt * nbp * 1024 + lane * 16;
+  const int snt = min(ng * 8 + 2 * (wave & 3) + (lane >> 5), ntiles - 1);
+  const uint8_t* ssrc = reinterpret_cast<const uint8_t*>(sc) + (size_t)snt * nbp * 128 + (lane & 31) * 4;
+
+  auto issue = [&](int h) {
+    const int bp = h >> 1, blk = h & 1;
+    uint8_t* base = smem + (h >> 1 & 1) * G::PAIR + blk * (G::AH + G::BH);
+#pragma unroll
+    for (int f = 0; f < FR; ++f)
+      glds16(asrc + (size_t)bp * CHUNK + (blk * FR + f) * 1024, base + wave * (FR * 1024) + f * 1024);
+    if (blk == 0) {
+      glds16(nsrc + (size_t)bp * 1024, base + G::AH + wave * 1024);
+      glds4(ssrc + (size_t)bp * 128, base + G::AH + 8192 + wave * 256);
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.0f;
+
+  u32x4 braw[TN];   // this wave's nibbles of the block pair (both blocks)
+  uint32_t bsc[TN]; // and its column's two f16 scales
+
+  // one half step: Q4 block 2 bp + BLK out of the slot at `base`
+  auto compute = [&](const uint8_t* base, auto blk_c) {
+    constexpr int BLK = decltype(blk_c)::value;
+    if constexpr (BLK == 0) {
+#pragma unroll
+      for (int nt = 0; nt < TN; ++nt) {
+        braw[nt] = *reinterpret_cast<const u32x4*>(base + G::AH + (wn * TN + nt) * 1024 + lane * 16);
+        bsc[nt] = *reinterpret_cast<const uint32_t*>(base + G::AH + 8192 + wn * 256 + nt * 128 + r * 4);
+      }
+    }
+    half8 qf[TN][2];
+    float dsc[TN];
+#pragma unroll
+    for (int nt = 0; nt < TN; ++nt) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        qf[nt][kk] = WQ4_WIDE_DIAG == 2 ? __builtin_bit_cast(half8, braw[nt]) : deq8(braw[nt][BLK * 2 + kk]);
+      dsc[nt] = (float)__builtin_bit_cast(_Float16, (uint16_t)(BLK ? (bsc[nt] >> 16) : (bsc[nt] & 0xffffu)));
+    }
+    auto chain = [&](const half8 (&ah)[2], const half8 (&al)[2], int nt) {
+      floatx16 t = mfma32(ah[0], qf[nt][0], floatx16{});
+      if constexpr (NS == 2) t = mfma32(al[0], qf[nt][0], t);
+      t = mfma32(ah[1], qf[nt][1], t);
+      if constexpr (NS == 2) t = mfma32(al[1], qf[nt][1], t);
+      return t;
+    };
+#if WQ4_WIDE_DIAG
+    floatx16 t0, t1;
+#pragma unroll
+    for (int mt = 0; mt < TM; ++mt) {
+      const uint8_t* fa = base + (wm * TM + mt) * (FR * 1024) + lane * 16;
+      half8 ahi[2], alo[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        ahi[kk] = *reinterpret_cast<const half8*>(fa + kk * NS * 1024);
+        if constexpr (NS == 2) alo[kk] = *reinterpret_cast<const half8*>(fa + kk * NS * 1024 + 1024);
+      }
+      (void)t0;
+      (void)t1;
+#pragma unroll
+      for (int nt = 0; nt < TN; ++nt) {
+        acc[mt][nt] = mfma32(ahi[0], qf[nt][0], acc[mt][nt]);
+        if constexpr (NS == 2) acc[mt][nt] = mfma32(alo[0], qf[nt][0], acc[mt][nt]);
+        acc[mt][nt] = mfma32(ahi[1], qf[nt][1], acc[mt][nt]);
+        if constexpr (NS == 2) acc[mt][nt] = mfma32(alo[1], qf[nt][1], acc[mt][nt]);
+      }
+    }
+    asm volatile("" ::"v"(dsc[0]), "v"(dsc[1]));
+#elif WQ4_WIDE_SCHED == 0
+    // two temporaries in flight: tile (mt, 1)'s MFMA chain runs under the
+    // scale FMAs of (mt, 0), and (mt + 1, 0)'s under those of (mt, 1)
+    floatx16 t0, t1;
+#pragma unroll
+    for (int mt = 0; mt < TM; ++mt) {
+      const uint8_t* fa = base + (wm * TM + mt) * (FR * 1024) + lane * 16;
+      half8 ahi[2], alo[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        ahi[kk] = *reinterpret_cast<const half8*>(fa + kk * NS * 1024);
+        if constexpr (NS == 2) alo[kk] = *reinterpret_cast<const half8*>(fa + kk * NS * 1024 + 1024);
+      }
+      t0 = chain(ahi, alo, 0);
+      if (mt > 0) acc[mt - 1][1] = t1 * dsc[1] + acc[mt - 1][1];
+      t1 = chain(ahi, alo, 1);
+      acc[mt][0] = t0 * dsc[0] + acc[mt][0];
+    }
+    acc[TM - 1][1] = t1 * dsc[1] + acc[TM - 1][1];
+#elif WQ4_WIDE_SCHED == 1
+    // Tiles j = 0..7 (m-tile j / 2, n-tile j % 2) through three rotating
+    // temporaries: between the MFMAs of tile j's chain sit the scale FMAs of
+    // tile j - 2 (a chain two tiles old has completed: no FMA waits on an
+    // MFMA) and, in the first chain of each m-tile, the reads of the next
+    // m-tile's A fragments; sched_barrier pins that order (left to itself
+    // the scheduler bunches the FMAs behind the MFMAs, and the two waves of
+    // a SIMD then idle the matrix pipe together).  Same per-element
+    // arithmetic in the same order: the tile kernel's bits.
+    constexpr int NM = 2 * NS;        // MFMAs per chain
+    constexpr int FPM = 16 / NM;      // scale FMAs (elements) per MFMA
+    floatx16 tt[3];
+    half8 a[2][2][NS];  // [m-tile parity][kk][hi, lo]
+    auto afrag = [&](int mt, int kk, int q) {
+      return *reinterpret_cast<const half8*>(base + (wm * TM + mt) * (FR * 1024) + (kk * NS + q) * 1024 + lane * 16);
+    };
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int q = 0; q < NS; ++q) a[0][kk][q] = afrag(0, kk, q);
+#pragma unroll
+    for (int j = 0; j < 2 * TM; ++j) {
+      const int mt = j >> 1, nt = j & 1, pb = mt & 1;
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        const int kk = i / NS, q = i % NS;
+        tt[j % 3] = mfma32(a[pb][kk][q], qf[nt][kk], i == 0 ? floatx16{} : tt[j % 3]);
+        if (nt == 0 && mt + 1 < TM) a[pb ^ 1][kk][q] = afrag(mt + 1, kk, q);
+        if (j >= 2) {
+          const int p = j - 2;
+#pragma unroll
+          for (int e = i * FPM; e < (i + 1) * FPM; ++e)
+            acc[p >> 1][p & 1][e] = __builtin_fmaf(tt[p % 3][e], dsc[p & 1], acc[p >> 1][p & 1][e]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int p = 2 * TM - 2; p < 2 * TM; ++p)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        acc[p >> 1][p & 1][e] = __builtin_fmaf(tt[p % 3][e], dsc[p & 1], acc[p >> 1][p & 1][e]);
+#else
+    // WQ4_WIDE_SCHED == 2: the order of WQ4_WIDE_SCHED == 1, pinned by
+    // writing each MFMA together with the scale FMAs that ride behind it as
+    // one asm statement (grp_mfma_fma): asm statements keep their order, and
+    // hipcc cannot pull the FMAs together behind the MFMAs.  Hazards inside
+    // the statements (hipcc pads none, cdna_hip_programming.md §5.7): an FMA
+    // reads a temporary whose chain ended >= 2 NS statements (>= 12 states)
+    // earlier; the first MFMA on a freshly dequantised B operand opens with
+    // s_nop 1; a chain's MFMAs accumulate in place (0 states).
+    // (f16 operands, NS = 1: the plain loop)
+    if constexpr (NS == 1) {
+      floatx16 t0, t1;
+#pragma unroll
+      for (int mt = 0; mt < TM; ++mt) {
+        const uint8_t* fa = base + (wm * TM + mt) * (FR * 1024) + lane * 16;
+        half8 ahi[2], alo[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) ahi[kk] = *reinterpret_cast<const half8*>(fa + kk * NS * 1024);
+        t0 = chain(ahi, alo, 0);
+        if (mt > 0) acc[mt - 1][1] = t1 * dsc[1] + acc[mt - 1][1];
+        t1 = chain(ahi, alo, 1);
+        acc[mt][0] = t0 * dsc[0] + acc[mt][0];
+      }
+      acc[TM - 1][1] = t1 * dsc[1] + acc[TM - 1][1];
+      return;
+    }
+    floatx16 tt[3];
+    half8 a[2][2][2];  // [m-tile parity][kk][hi, lo]
+    auto afrag = [&](int mt, int kk, int q) {
+      return *reinterpret_cast<const half8*>(base + (wm * TM + mt) * (FR * 1024) + (kk * NS + q) * 1024 + lane * 16);
+    };
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) a[0][kk][q] = afrag(0, kk, q);
+#pragma unroll
+    for (int j = 0; j < 2 * TM; ++j) {
+      const int mt = j >> 1, nt = j & 1, pb = mt & 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int kk = i >> 1, q = i & 1;
+        if (j >= 2) {
+          const int p = j - 2;
+          floatx16& c = acc[p >> 1][p & 1];
+          const floatx16& t = tt[p % 3];
+          float c0 = c[4 * i], c1 = c[4 * i + 1], c2 = c[4 * i + 2], c3 = c[4 * i + 3];
+          grp_mfma_fma(tt[j % 3], a[pb][kk][q], qf[nt][kk], i == 0, false, c0, c1, c2, c3, t[4 * i], t[4 * i + 1],
+                       t[4 * i + 2], t[4 * i + 3], dsc[p & 1]);
+          c[4 * i] = c0;
+          c[4 * i + 1] = c1;
+          c[4 * i + 2] = c2;
+          c[4 * i + 3] = c3;
+        } else {
+          grp_mfma(tt[j % 3], a[pb][kk][q], qf[nt][kk], i == 0, i == 0);
+        }
+        if (nt == 0 && mt + 1 < TM) a[pb ^ 1][kk][q] = afrag(mt + 1, kk, q);
+      }
+    }
+#pragma unroll
+    for (int p = 2 * TM - 2; p < 2 * TM; ++p)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        acc[p >> 1][p & 1][e] = __builtin_fmaf(tt[p % 3][e], dsc[p & 1], acc[p >> 1][p & 1][e]);
+#endif
+  };
+
+  const int H = 2 * nbp;
+#if WQ4_WIDE_STAMP
+  unsigned long long st_acc[4] = {0, 0, 0, 0}, st_t = 0;
+  const unsigned long long st_begin = __builtin_amdgcn_s_memtime();
+#define WIDE_STAMP(k)                                            \
+  {                                                              \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    if (k >= 0) st_acc[k < 0 ? 0 : k] += now_ - st_t;            \
+    st_t = now_;                                                 \
+  }
+#else
+#define WIDE_STAMP(k)
+#endif
+  issue(0);
+  if (H > 1) issue(1);
+  if (H > 2) issue(2);
+  for (int bp = 0; bp < nbp; ++bp) {
+    const bool more = bp + 1 < nbp;
+    const uint8_t* b0 = smem + (bp & 1) * G::PAIR;
+    // even half step: block 2 bp (slot 2 (bp & 1))
+    WIDE_STAMP(-1);
+    if (more) vm_wait<G::CNT0 + G::CNT1>();
+    else vm_wait<G::CNT1>();
+    WIDE_STAMP(0);
+    ring_barrier();
+    WIDE_STAMP(1);
+    if (more) issue(2 * bp + 3);
+    WIDE_STAMP(2);
+    if (active) compute(b0, std::integral_constant<int, 0>{});
+    WIDE_STAMP(3);
+    // odd half step: block 2 bp + 1 (slot 2 (bp & 1) + 1)
+    if (more) vm_wait<G::CNT0 + G::CNT1>();
+    else vm_wait<0>();
+    WIDE_STAMP(0);
+    ring_barrier();
+    WIDE_STAMP(1);
+    if (2 * bp + 4 < H) issue(2 * bp + 4);
+    WIDE_STAMP(2);
+    if (active) compute(b0 + G::AH + G::BH, std::integral_constant<int, 1>{});
+    WIDE_STAMP(3);
+  }
+#undef WIDE_STAMP
+  __syncthreads();  // the ring is drained and read: the epilogue stage may reuse it
+#if WQ4_WIDE_STAMP
+  if (lane == 0 && (wave == 0 || wave == 4) && blockIdx.x < kWideStampWgs) {
+    unsigned long long* o = g_wide_stamps + ((size_t)blockIdx.x * 2 + (wave >> 2)) * 5;
+    for (int k = 0; k < 4; ++k) o[k] = st_acc[k];
+    o[4] = __builtin_amdgcn_s_memtime() - st_begin;
+  }
+#endif
+
+  tile_epilogue<NS, EPI, TM, TN>(acc, mg * 8 + wm * TM, nt0, active, mtiles, colscale,
+                                 reinterpret_cast<float*>(smem) + wave * (32 * kStageLd), lane, e);
+}
+
+bool wide_gemm_supported(const Q4Geom& g, int rows, int ns, int wtype) {
+  return wtype == kWeightsQ4 && (ns == 1 || ns == 2) && rows > 128 && g.kb >= 1 && g.ntiles % 2 == 0;
+}
+
+template <int NS>
+static hipError_t launch_wide_t(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* cs,
+                                const _Float16* at, int rows, const EpiArgs& e, int epi_mode, hipStream_t st) {
+  const int mtiles = (int)(round_up(rows < 1 ? 1 : rows, kMPad) / kMTile);
+  const int ngroups = (int)((g.ntiles + 7) / 8);
+  const int mgroups = (mtiles + 7) / 8;
+  const dim3 grid((unsigned)(ngroups * mgroups));
+  const size_t lds = WideGeo<NS>::LDS;
+  if (epi_mode == kEpiTiled)
+    hipLaunchKernelGGL((q4_gemm_wide_kernel<NS, kEpiTiled>), grid, dim3(512), lds, st, nib, sc, cs, at, mtiles,
+                       (int)g.nbp, (int)g.ntiles, e);
+  else if (epi_mode == kEpiHeadMajor)
+    hipLaunchKernelGGL((q4_gemm_wide_kernel<NS, kEpiHeadMajor>), grid, dim3(512), lds, st, nib, sc, cs, at, mtiles,
+                       (int)g.nbp, (int)g.ntiles, e);
+  else
+    hipLaunchKernelGGL((q4_gemm_wide_kernel<NS, kEpiF32>), grid, dim3(512), lds, st, nib, sc, cs, at, mtiles,
+                       (int)g.nbp, (int)g.ntiles, e);
+  return hipGetLastError();
+}
+
+hipError_t launch_wide_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t* sc, const float* cs,
+                            const _Float16* at, int rows, const EpiArgs& e, int epi_mode, int ns, hipStream_t st) {
+  if (ns == 2) return launch_wide_t<2>(g, nib, sc, cs, at, rows, e, epi_mode, st);
+  return launch_wide_t<1>(g, nib, sc, cs, at, rows, e, epi_mode, st);
+}
+
+}  // namespace wq4
+
+// Timing diagnostics (WQ4_WIDE_STAMP builds only; 0 workgroups otherwise):
+// copies [wgs][2 waves][5] loop-phase cycle sums of the last wide launch.
+extern "C" int wq4_diag_wide_stamps(unsigned long long* out, int max_wgs) {
+#if WQ4_WIDE_STAMP
+  const int n = max_wgs < wq4::kWideStampWgs ? max_wgs : wq4::kWideStampWgs;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(wq4::g_wide_stamps), (size_t)n * 2 * 5 * sizeof(unsigned long long)) !=
+      hipSuccess)
+    return -1;
+  return n;
+#else
+  (void)out;
+  (void)max_wgs;
+  return 0;
+#endif
+}
