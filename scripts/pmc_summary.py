@@ -21,7 +21,8 @@ import os
 import re
 import sys
 
-FAMILIES = {"q4_gemm_prefill_kernel": r"q4_gemm_prefill_kernel", "q4_gemm_decode_kernel": r"q4_gemm_decode_kernel",
+FAMILIES = {"q4_gemm_prefill_kernel": r"q4_gemm_prefill_kernel", "q4_gemm_wide_kernel": r"q4_gemm_wide_kernel",
+            "q4_gemm_decode_kernel": r"q4_gemm_decode_kernel",
             "xattn_main_kernel": r"xattn_main_kernel",
             "xattn_q_kernel": r"xattn_q_\w*kernel", "xattn_merge_kernel": r"xattn_merge_kernel",
             "xattn_out_kernel": r"xattn_out_kernel"}

@@ -41,16 +41,17 @@ def main():
         torch.cuda.synchronize()
         mg, ng = (-(-M // 32) + 7) // 8, (n // 32 + 7) // 8
         wgs = min(mg * ng, 4096)
-        buf = (ctypes.c_ulonglong * (wgs * 10))()
+        buf = (ctypes.c_ulonglong * (wgs * 12))()
         got = L.wq4_diag_wide_stamps(buf, wgs)
-        a = np.frombuffer(buf, dtype=np.uint64).reshape(wgs, 2, 5).astype(np.float64)[:got]
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(wgs, 2, 6).astype(np.float64)[:got]
         tot = a[:, :, 4]
         halves = 2 * ((k // 32 + 1) // 2)
         for w, name in ((0, "wave 0"), (1, "wave 4")):
             fr = a[:, w, :4].sum(0) / tot[:, w].sum()
             print(f"N={n:5d} K={k:5d} {name}: vmcnt {fr[0]:.3f} barrier {fr[1]:.3f} issue {fr[2]:.3f} "
                   f"compute {fr[3]:.3f}; {np.median(tot[:, w]) / halves:7.0f} cycles per half step "
-                  f"(compute {np.median(a[:, w, 3]) / halves:6.0f})", flush=True)
+                  f"(compute {np.median(a[:, w, 3]) / halves:6.0f}); clock {np.median(tot[:, w] / a[:, w, 5]) * 0.1:.2f} GHz",
+                  flush=True)
 
 
 if __name__ == "__main__":

@@ -377,23 +377,27 @@ static std::atomic<int> g_enc_mode{[] {
 }()};
 
 // Which kernel runs a rows > 128 Q4_0 GEMM: 0 = the prefill tile kernel,
-// 2 = the ring kernel's L geometry, 3 = its S geometry.  Measured (r03,
-// tools/enc_ab.py, Large-V3 encoder shapes): at M = 48000 the tile kernel
-// (433-499 TF/s) and L (430-494) are equal within noise -- both sit at the
-// same ~1,000 TF/s of MFMA work, the block-scale FMAs costing ~20 % of it
-// (encdiag builds) -- while at one clip (M = 1500) the tile kernel's 60-240
-// workgroups leave the chip idle and S runs 1.1-2.4x faster (one layer's
-// four GEMMs 0.191 vs 0.349 ms).  Crossover measured at M = 1500, 3000,
-// 6000, 12000 (profiles/r03_enc_ab.log): S while the tile kernel's grid has
-// < 400 workgroups, the tile kernel above.
+// 2 = the ring kernel's L geometry, 3 = its S geometry, 5 = the 8-wave wide
+// kernel (wq4_wide.hip).  Measured (r03, tools/enc_ab.py, Large-V3 encoder
+// shapes): at M = 1500 the tile kernel's 60-240 workgroups leave the chip
+// idle and S runs 1.1-2.4x faster (one layer's four GEMMs 0.191 vs 0.349
+// ms); crossover at M = 1500, 3000, 6000, 12000 (profiles/r03_enc_ab.log):
+// S while the tile kernel's grid has < 400 workgroups.  r06
+// (profiles/r06_enc_ab_rows.log, tile vs wide interleaved in one process):
+// at M = 48000 the wide kernel is 1-7 % faster on every shape (457 / 454 /
+// 488 / 562 TF/s against 453 / 424 / 471 / 530), at 24000 and 12000 on 7 of
+// 8, at 6000 only where its own grid is >= 480 workgroups: wide while its
+// 256 x 256 grid has >= 400 workgroups.
 int enc_gemm_pick(const Q4Geom& g, int rows, int epi_mode, int ns, int wtype) {
   const int mode = g_enc_mode.load();
   if (mode == 0 || wtype != kWeightsQ4 || rows <= 128 || g.kb < 1) return 0;
   if (mode == 5) return wide_gemm_supported(g, rows, ns, wtype) ? 5 : 0;
-  if (ns != 2) return 0;  // the ring kernel: f16x2 operands only
-  if (mode >= 2) return mode;
   const int64_t mt = round_up(rows, kMPad) / kMTile;
   const int64_t tile_grid = ((mt + 3) / 4) * ((g.ntiles + 7) / 8);
+  const int64_t wide_grid = ((mt + 7) / 8) * ((g.ntiles + 7) / 8);
+  if (mode == 1 && wide_grid >= 400 && wide_gemm_supported(g, rows, ns, wtype)) return 5;
+  if (ns != 2) return 0;  // the ring kernel: f16x2 operands only
+  if (mode >= 2) return mode;
   return tile_grid < 400 ? 3 : 0;
 }
 

@@ -51,7 +51,7 @@ namespace wq4 {
 #endif
 constexpr int kWideStampWgs = 4096;
 #if WQ4_WIDE_STAMP
-__device__ unsigned long long g_wide_stamps[kWideStampWgs * 2 * 5];
+__device__ unsigned long long g_wide_stamps[kWideStampWgs * 2 * 6];
 #endif
 
 // WQ4_WIDE_SCHED: the half step's instruction order (A/B builds): 0 the
@@ -60,6 +60,11 @@ __device__ unsigned long long g_wide_stamps[kWideStampWgs * 2 * 5];
 // statements (one MFMA + its scale FMAs each).
 #ifndef WQ4_WIDE_SCHED
 #define WQ4_WIDE_SCHED 2
+#endif
+// WQ4_WIDE_SPREAD (with WQ4_WIDE_SCHED 2): the next half step's LDS-DMA
+// copies issued one per MFMA chain (1) instead of all after the barrier (0).
+#ifndef WQ4_WIDE_SPREAD
+#define WQ4_WIDE_SPREAD 1
 #endif
 
 // One MFMA of a block chain, t = A B + (first ? 0 : t); nop: open with
@@ -164,16 +169,20 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
   const int snt = min(ng * 8 + 2 * (wave & 3) + (lane >> 5), ntiles - 1);
   const uint8_t* ssrc = reinterpret_cast<const uint8_t*>(sc) + (size_t)snt * nbp * 128 + (lane & 31) * 4;
 
-  auto issue = [&](int h) {
+  // copy n (0 .. FR + 1) of half step h's CNT0 / CNT1 copies into its slot
+  auto issue_part = [&](int h, int n) {
     const int bp = h >> 1, blk = h & 1;
     uint8_t* base = smem + (h >> 1 & 1) * G::PAIR + blk * (G::AH + G::BH);
-#pragma unroll
-    for (int f = 0; f < FR; ++f)
-      glds16(asrc + (size_t)bp * CHUNK + (blk * FR + f) * 1024, base + wave * (FR * 1024) + f * 1024);
-    if (blk == 0) {
+    if (n < FR)
+      glds16(asrc + (size_t)bp * CHUNK + (blk * FR + n) * 1024, base + wave * (FR * 1024) + n * 1024);
+    else if (blk == 0 && n == FR)
       glds16(nsrc + (size_t)bp * 1024, base + G::AH + wave * 1024);
+    else if (blk == 0 && n == FR + 1)
       glds4(ssrc + (size_t)bp * 128, base + G::AH + 8192 + wave * 256);
-    }
+  };
+  auto issue = [&](int h) {
+#pragma unroll
+    for (int n = 0; n < FR + 2; ++n) issue_part(h, n);
   };
 
   floatx16 acc[TM][TN];
@@ -188,8 +197,13 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
   uint32_t bsc[TN]; // and its column's two f16 scales
 
   // one half step: Q4 block 2 bp + BLK out of the slot at `base`
-  auto compute = [&](const uint8_t* base, auto blk_c) {
+  // pend >= 0: the half step whose LDS-DMA copies this one issues (into the
+  // slot the barrier freed); the pinned schedule spreads them over its
+  // first chains, the other forms issue them up front
+  auto compute = [&](const uint8_t* base, auto blk_c, int pend) {
     constexpr int BLK = decltype(blk_c)::value;
+    constexpr bool kSpread = WQ4_WIDE_SPREAD && WQ4_WIDE_SCHED == 2 && NS == 2 && !WQ4_WIDE_DIAG;
+    if (!kSpread && pend >= 0) issue(pend);
     if constexpr (BLK == 0) {
 #pragma unroll
       for (int nt = 0; nt < TN; ++nt) {
@@ -352,6 +366,7 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
           grp_mfma(tt[j % 3], a[pb][kk][q], qf[nt][kk], i == 0, i == 0);
         }
         if (nt == 0 && mt + 1 < TM) a[pb ^ 1][kk][q] = afrag(mt + 1, kk, q);
+        if (kSpread && i == 1 && j < FR + 2 && pend >= 0) issue_part(pend, j);  // one copy per chain
       }
     }
 #pragma unroll
@@ -366,6 +381,7 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
 #if WQ4_WIDE_STAMP
   unsigned long long st_acc[4] = {0, 0, 0, 0}, st_t = 0;
   const unsigned long long st_begin = __builtin_amdgcn_s_memtime();
+  const unsigned long long st_rbegin = __builtin_amdgcn_s_memrealtime();
 #define WIDE_STAMP(k)                                            \
   {                                                              \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
@@ -388,9 +404,9 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
     WIDE_STAMP(0);
     ring_barrier();
     WIDE_STAMP(1);
-    if (more) issue(2 * bp + 3);
     WIDE_STAMP(2);
-    if (active) compute(b0, std::integral_constant<int, 0>{});
+    if (active) compute(b0, std::integral_constant<int, 0>{}, more ? 2 * bp + 3 : -1);
+    else if (more) issue(2 * bp + 3);
     WIDE_STAMP(3);
     // odd half step: block 2 bp + 1 (slot 2 (bp & 1) + 1)
     if (more) vm_wait<G::CNT0 + G::CNT1>();
@@ -398,18 +414,19 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
     WIDE_STAMP(0);
     ring_barrier();
     WIDE_STAMP(1);
-    if (2 * bp + 4 < H) issue(2 * bp + 4);
     WIDE_STAMP(2);
-    if (active) compute(b0 + G::AH + G::BH, std::integral_constant<int, 1>{});
+    if (active) compute(b0 + G::AH + G::BH, std::integral_constant<int, 1>{}, 2 * bp + 4 < H ? 2 * bp + 4 : -1);
+    else if (2 * bp + 4 < H) issue(2 * bp + 4);
     WIDE_STAMP(3);
   }
 #undef WIDE_STAMP
   __syncthreads();  // the ring is drained and read: the epilogue stage may reuse it
 #if WQ4_WIDE_STAMP
   if (lane == 0 && (wave == 0 || wave == 4) && blockIdx.x < kWideStampWgs) {
-    unsigned long long* o = g_wide_stamps + ((size_t)blockIdx.x * 2 + (wave >> 2)) * 5;
+    unsigned long long* o = g_wide_stamps + ((size_t)blockIdx.x * 2 + (wave >> 2)) * 6;
     for (int k = 0; k < 4; ++k) o[k] = st_acc[k];
     o[4] = __builtin_amdgcn_s_memtime() - st_begin;
+    o[5] = __builtin_amdgcn_s_memrealtime() - st_rbegin;  // 100 MHz ticks
   }
 #endif
 
@@ -450,11 +467,12 @@ hipError_t launch_wide_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t*
 }  // namespace wq4
 
 // Timing diagnostics (WQ4_WIDE_STAMP builds only; 0 workgroups otherwise):
-// copies [wgs][2 waves][5] loop-phase cycle sums of the last wide launch.
+// copies [wgs][2 waves][6] loop-phase cycle sums of the last wide launch
+// (vmcnt, barrier, issue, compute, loop total; then the loop's s_memrealtime).
 extern "C" int wq4_diag_wide_stamps(unsigned long long* out, int max_wgs) {
 #if WQ4_WIDE_STAMP
   const int n = max_wgs < wq4::kWideStampWgs ? max_wgs : wq4::kWideStampWgs;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(wq4::g_wide_stamps), (size_t)n * 2 * 5 * sizeof(unsigned long long)) !=
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(wq4::g_wide_stamps), (size_t)n * 2 * 6 * sizeof(unsigned long long)) !=
       hipSuccess)
     return -1;
   return n;
