@@ -58,6 +58,7 @@ __device__ __forceinline__ floatx16 mfma_f32(float a, float b, const floatx16& c
 }
 
 using wq4::atile_store4;
+using wq4::attn_store4;
 using wq4::kbp_of;
 using wq4::split_f16;
 
@@ -109,7 +110,8 @@ constexpr int kEaLd = 72;    // LDS row stride (halves)
 template <int NS, int NW>
 __global__ __launch_bounds__(64 * NW, WA_EA_WAVES) void encoder_attention_f16_kernel(const float* __restrict__ qkv,
                                                                                     int T, int H,
-                                                                                    _Float16* __restrict__ tiled) {
+                                                                                    _Float16* __restrict__ tiled,
+                                                                                    float* __restrict__ out32) {
   // two tile buffers: tile kt + 1 is staged into the other one while tile
   // kt is read, one barrier per tile
   __shared__ __attribute__((aligned(16))) _Float16 klsb[2][NS][kEaKeys * kEaLd];
@@ -316,14 +318,14 @@ __global__ __launch_bounds__(64 * NW, WA_EA_WAVES) void encoder_attention_f16_ke
 #pragma unroll
       for (int gg = 0; gg < 4; ++gg) {
         const int d = dt * 32 + 8 * gg + 4 * lh;
-        atile_store4<NS>(tiled, row, head * 64 + d, kbp, o[dt][4 * gg] * inv, o[dt][4 * gg + 1] * inv,
-                         o[dt][4 * gg + 2] * inv, o[dt][4 * gg + 3] * inv);
+        attn_store4<NS>(tiled, out32, H * 64, row, head * 64 + d, kbp, o[dt][4 * gg] * inv,
+                        o[dt][4 * gg + 1] * inv, o[dt][4 * gg + 2] * inv, o[dt][4 * gg + 3] * inv);
       }
   }
 }
 
 hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Float16* tiled, int ns,
-                                    hipStream_t st) {
+                                    hipStream_t st, float* out32) {
   // 8 waves x 32 queries per workgroup; when that grid leaves most CUs idle
   // (one or two clips: 120 / 240 workgroups at Large-V3) 4 waves, twice the
   // workgroups (each query's arithmetic is the same either way)
@@ -331,16 +333,16 @@ hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Floa
   if (few) {
     const dim3 g4((T + 127) / 128, H, B);
     if (ns == 2)
-      hipLaunchKernelGGL((encoder_attention_f16_kernel<2, 4>), g4, dim3(256), 0, st, qkv, T, H, tiled);
+      hipLaunchKernelGGL((encoder_attention_f16_kernel<2, 4>), g4, dim3(256), 0, st, qkv, T, H, tiled, out32);
     else
-      hipLaunchKernelGGL((encoder_attention_f16_kernel<1, 4>), g4, dim3(256), 0, st, qkv, T, H, tiled);
+      hipLaunchKernelGGL((encoder_attention_f16_kernel<1, 4>), g4, dim3(256), 0, st, qkv, T, H, tiled, out32);
     return hipGetLastError();
   }
   const dim3 g2((T + 255) / 256, H, B);
   if (ns == 2)
-    hipLaunchKernelGGL((encoder_attention_f16_kernel<2, 8>), g2, dim3(512), 0, st, qkv, T, H, tiled);
+    hipLaunchKernelGGL((encoder_attention_f16_kernel<2, 8>), g2, dim3(512), 0, st, qkv, T, H, tiled, out32);
   else
-    hipLaunchKernelGGL((encoder_attention_f16_kernel<1, 8>), g2, dim3(512), 0, st, qkv, T, H, tiled);
+    hipLaunchKernelGGL((encoder_attention_f16_kernel<1, 8>), g2, dim3(512), 0, st, qkv, T, H, tiled, out32);
   return hipGetLastError();
 }
 
@@ -473,7 +475,7 @@ template <int NS, int TQ>
 __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restrict__ qkv, float* __restrict__ ck,
                                                             float* __restrict__ cv, int Tq_, int H, int ctx,
                                                             const DecodeState* state, int kv_len_host,
-                                                            _Float16* __restrict__ tiled) {
+                                                            _Float16* __restrict__ tiled, float* __restrict__ out32) {
   const int Tq = TQ == 1 ? 1 : Tq_;
   __shared__ float wm[4][TQ], wl[4][TQ];
   __shared__ float wo[4][TQ][64];
@@ -523,18 +525,18 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(const float* __restr
     const int t = wave;
     const float val = os / ls;
     const float v1 = __shfl_down(val, 1, 64), v2 = __shfl_down(val, 2, 64), v3 = __shfl_down(val, 3, 64);
-    if ((lane & 3) == 0) atile_store4<NS>(tiled, b * Tq + t, head * 64 + lane, kbp_of(D), val, v1, v2, v3);
+    if ((lane & 3) == 0) attn_store4<NS>(tiled, out32, D, b * Tq + t, head * 64 + lane, kbp_of(D), val, v1, v2, v3);
   }
 }
 
 hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float* cache_v, int B, int Tq, int H,
                                          int ctx, const DecodeState* state, int kv_len_host, _Float16* tiled,
-                                         int ns, hipStream_t st) {
+                                         int ns, hipStream_t st, float* out32) {
   if (Tq > 4 || ctx > kMaxCtx) return hipErrorInvalidValue;
   const dim3 grid(H, B), block(256);
 #define WA_SELF(NS_, TQ_)                                                                                     \
   hipLaunchKernelGGL((dec_self_attn_kernel<NS_, TQ_>), grid, block, 0, st, qkv, cache_k, cache_v, Tq, H, ctx, \
-                     state, kv_len_host, tiled)
+                     state, kv_len_host, tiled, out32)
   if (ns == 2) {
     if (Tq == 1) { WA_SELF(2, 1); } else { WA_SELF(2, 4); }
   } else {
@@ -578,7 +580,7 @@ __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restr
                                                             const float* __restrict__ vc, int Tq_, int T, int H,
                                                             int S, float* __restrict__ part,
                                                             int* __restrict__ counters,
-                                                            _Float16* __restrict__ tiled) {
+                                                            _Float16* __restrict__ tiled, float* __restrict__ out32) {
   constexpr int U = TQ == 1 ? 12 : 8;  // <= 48 keys per wave in flight at once (decode step)
   const int Tq = TQ == 1 ? 1 : Tq_;
   __shared__ float wm[4][TQ], wl[4][TQ];
@@ -665,7 +667,7 @@ __global__ __launch_bounds__(256) void cross_attn_kv_kernel(const float* __restr
     const int t = wave;
     const float val = os / ls;
     const float v1 = __shfl_down(val, 1, 64), v2 = __shfl_down(val, 2, 64), v3 = __shfl_down(val, 3, 64);
-    if ((lane & 3) == 0) atile_store4<NS>(tiled, b * Tq + t, head * 64 + lane, kbp_of(D), val, v1, v2, v3);
+    if ((lane & 3) == 0) attn_store4<NS>(tiled, out32, D, b * Tq + t, head * 64 + lane, kbp_of(D), val, v1, v2, v3);
   }
 }
 
@@ -674,13 +676,14 @@ size_t cross_attention_kv_part_floats(int B, int H, int T) {
 }
 
 hipError_t launch_cross_attention_kv(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
-                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st) {
+                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st,
+                                     float* out32) {
   if (Tq < 1 || Tq > 4 || B < 1 || T < 1 || H < 1 || !q) return hipErrorInvalidValue;
   const int S = cross_attention_kv_splits(T);
   const dim3 grid(H * S, B), block(256);
 #define WA_XKV(NS_, TQ_)                                                                                           \
   hipLaunchKernelGGL((cross_attn_kv_kernel<NS_, TQ_>), grid, block, 0, st, q, k, v, Tq, T, H, S, part, counters, \
-                     tiled)
+                     tiled, out32)
   if (ns == 2) {
     if (Tq == 1) { WA_XKV(2, 1); } else { WA_XKV(2, 4); }
   } else {

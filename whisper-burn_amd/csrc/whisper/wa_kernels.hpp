@@ -18,9 +18,11 @@ struct DecodeState {
 
 // Encoder self-attention (attention.rs:243-298, non-causal), flash-style,
 // f32 MFMA.  qkv: [B*T, 3D] f32 (q | k | v).  Writes the A-tiled operand of
-// the output projection (rows b*T + t, K = D).
+// the output projection (rows b*T + t, K = D) -- or, with out32 non-null
+// (range tier 3, wa_model), f32 rows [B*T][D] there instead.  The same holds
+// for every attention launcher below.
 hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Float16* tiled, int ns,
-                                    hipStream_t st);
+                                    hipStream_t st, float* out32 = nullptr);
 
 // Decoder self-attention with KV cache (attention.rs:62-125).  qkv [B*Tq, 3D];
 // appends k, v of the Tq new tokens at cache index kv_len (+ kv_base_extra)
@@ -28,7 +30,7 @@ hipError_t launch_encoder_attention(const float* qkv, int B, int T, int H, _Floa
 // Tq > 1 (attention.rs:270-287).  cache_k/v: [B, ctx, D].
 hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float* cache_v, int B, int Tq, int H,
                                          int ctx, const DecodeState* state, int kv_len_host, _Float16* tiled,
-                                         int ns, hipStream_t st);
+                                         int ns, hipStream_t st, float* out32 = nullptr);
 
 // Cross-attention over cached K / V (attention.rs:177-236, the reference's
 // form; used for decode groups of a few clips): q [B*Tq, D] f32, k / v
@@ -39,7 +41,8 @@ hipError_t launch_decoder_self_attention(const float* qkv, float* cache_k, float
 int cross_attention_kv_splits(int T);
 size_t cross_attention_kv_part_floats(int B, int H, int T);
 hipError_t launch_cross_attention_kv(const float* q, const float* k, const float* v, int B, int Tq, int T, int H,
-                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st);
+                                     float* part, int* counters, _Float16* tiled, int ns, hipStream_t st,
+                                     float* out32 = nullptr);
 
 // Cross-attention over the encoder output (wa_xattn.hip; attention.rs:
 // 204-298 restated without K/V caches): q [B*Tq, D] f32 (rows b*Tq + i),
@@ -61,7 +64,7 @@ hipError_t launch_wv_pack(const uint8_t* wv, int H, int D, uint32_t* out, hipStr
 // wvp: the launch_wv_pack words of wv (Q4 weights; ignored for f16 weights).
 hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, const uint32_t* wvp, const float* bv,
                         int wtype, const _Float16* enc, int B, int Tq, int T, int H, int D, _Float16* qt, float* part,
-                        _Float16* tiled, int ns, hipStream_t st);
+                        _Float16* tiled, int ns, hipStream_t st, float* out32 = nullptr);
 // A-tiled operand [R][K] (hi + lo) -> f32 rows (diagnostics).
 hipError_t launch_untile(const _Float16* tiled, int R, int K, int ns, float* out, hipStream_t st);
 // f32 rows [rows][D] -> [rows][ns][D] f16 planes (hi | lo) for launch_xattn.

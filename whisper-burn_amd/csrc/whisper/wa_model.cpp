@@ -261,6 +261,7 @@ struct wa_model {
   hipStream_t enc_stream = nullptr;
   int enc_cus = 0;
   int overlap_k = -1;
+  int overlap_b = 0, overlap_eot = -1;  // the batch shape overlap_k was adapted to
   float pipe[4] = {0, 0, 0, 0};
   // Activation-range guard.  Every internal producer writes MFMA operands as
   // f16 pairs of x * 2^4 (wq4_device.hpp split_act), finite for |x| < 4094;
@@ -279,6 +280,14 @@ struct wa_model {
   // reach fc2 finite.  Workspaces allocated when the tier is entered:
   // ffn_ws for the encoder's B * T rows, g.ffn_ws per decode group.
   bool wide_ffn = false;
+  // third tier (wide_ffn still flagged): every attention output (encoder
+  // self-attention, decoder self- and cross-attention) is written as f32
+  // rows instead of the f16-pair operand, and the output projections run as
+  // Q4Linear::forward at the ABI (wq4_linear_forward_ws: per-call operand
+  // scale).  Scratch: m->h1 (free during the encoder layers) / g.hid, with
+  // the layer's own A-tiled buffer as the ABI workspace.
+  bool wide_attn = false;
+  int range_tier() const { return wide_attn ? 3 : wide_ffn ? 2 : wide_range ? 1 : 0; }
   void* ffn_ws = nullptr;
   size_t ffn_ws_bytes = 0;
   float timings[5] = {0, 0, 0, 0, 0};
@@ -831,9 +840,12 @@ wq4_status encoder_layers(wa_model* m, int B, int l0, int l1, hipStream_t st) {
     }
     {
       Prof p(m, st, 1, 4.0 * B * H * (double)T * T * 64 * 1e-9, 16.0 * rows * D * 1e-9);
-      WA_HIP(wa::launch_encoder_attention(m->qkv, B, T, H, m->at_d, m->ns, st));
+      WA_HIP(wa::launch_encoder_attention(m->qkv, B, T, H, m->at_d, m->ns, st, m->wide_attn ? m->h1 : nullptr));
     }
-    {
+    if (m->wide_attn) {  // range tier 3: the f32 attention output through Q4Linear::forward (m->at_d: workspace)
+      WA_WQ4(wq4_linear_forward_ws(L.out, L.out_b, m->h1, m->x, m->x, rows, D, WQ4_EPI_RESIDUAL, m->prec, m->at_d,
+                                   wq4_atiled_bytes(rows, D, m->prec), st));
+    } else {
       Prof p = q4prof(m, st, L.out, rows);
       WA_WQ4(wq4_gemm_tiled(L.out, L.out_b, m->at_d, m->x, m->x, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 1, st));
     }
@@ -991,9 +1003,19 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
       WA_WQ4(wq4_layernorm(g.xd, L.ln1_w, L.ln1_b, rows, D, m->prec, g.atd_dec, nullptr, st));
       WA_WQ4(wq4_gemm_tiled(L.qkv, L.qkv_b, g.atd_dec, nullptr, g.qkvd, nullptr, rows, 0u, m->prec, 2, st));
     }
+    // range tier 3: attention outputs as f32 rows in g.hid, projected through
+    // Q4Linear::forward at the ABI (g.atd_dec: its workspace); tier >= 1 has
+    // the fold off
+    float* const a32 = m->wide_attn ? g.hid : nullptr;
+    const size_t a32_ws = wq4_atiled_bytes(rows, D, m->prec);
     WA_HIP(wa::launch_decoder_self_attention(g.qkvd, L.cache_k + self_ofs, L.cache_v + self_ofs, B, Tq, H,
-                                             c.n_text_ctx, state, kv0, g.atd_dec, m->ns, st));
-    if (fold) {
+                                             c.n_text_ctx, state, kv0, g.atd_dec, m->ns, st, a32));
+    if (a32) {
+      WA_WQ4(wq4_linear_forward_ws(L.out, L.out_b, a32, g.xd, g.xd, rows, D, WQ4_EPI_RESIDUAL, m->prec, g.atd_dec,
+                                   a32_ws, st));
+      WA_WQ4(wq4_layernorm(g.xd, L.ln2_w, L.ln2_b, rows, D, m->prec, g.atd_dec, nullptr, st));
+      WA_WQ4(wq4_gemm_tiled(L.cq, L.cq_b, g.atd_dec, nullptr, g.qd, nullptr, rows, 0u, m->prec, 2, st));
+    } else if (fold) {
       const wq4_ln_fold prod2{L.ln2_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
       WA_WQ4(wq4_gemm_tiled_lnfold(L.out, L.out_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec,
                                    &prod2, st));
@@ -1007,11 +1029,14 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
     if (m->group_kv(g)) {  // few clips: one GEMV launch over the cached K / V
       const size_t kofs = (size_t)g.b0 * T * D;
       WA_HIP(wa::launch_cross_attention_kv(g.qd, L.xk + kofs, L.xv + kofs, B, Tq, T, H, g.xkv_part, g.xkv_ctr,
-                                           g.atd_dec, m->ns, st));
+                                           g.atd_dec, m->ns, st, a32));
     } else {
       WA_HIP(wa::launch_xattn(g.qd, L.ck_raw, L.cv_raw, L.cv_p, L.cv_b, m->wtype, enc, B, Tq, T, H, D, g.xqt,
-                              g.xattn_part, g.atd_dec, m->ns, st));
+                              g.xattn_part, g.atd_dec, m->ns, st, a32));
     }
+    if (a32)  // range tier 3: the cross-attention output projection at the ABI
+      WA_WQ4(wq4_linear_forward_ws(L.cout, L.cout_b, a32, g.xd, g.xd, rows, D, WQ4_EPI_RESIDUAL, m->prec, g.atd_dec,
+                                   a32_ws, st));
     if (fold) {
       const wq4_ln_fold prod3{L.ln3_w, g.atd_ln, g.ln_stats, nullptr, nullptr};
       WA_WQ4(wq4_gemm_tiled_lnfold(L.cout, L.cout_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL,
@@ -1026,8 +1051,9 @@ wq4_status decoder_forward(wa_model* m, DecGroup& g, const int* tokens, int Tq, 
       WA_WQ4(wq4_gemm_tiled_lnfold(L.fc2, L.fc2_b, g.atf_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec,
                                    &prod1, st));
     } else {
-      WA_WQ4(wq4_gemm_tiled(L.cout, L.cout_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2,
-                            st));
+      if (!a32)
+        WA_WQ4(wq4_gemm_tiled(L.cout, L.cout_b, g.atd_dec, g.xd, g.xd, nullptr, rows, WQ4_EPI_RESIDUAL, m->prec, 2,
+                              st));
       if (m->wide_ffn) {  // range tier 2: Q4FFN::forward with per-call operand scales (g.hid: f32 scratch)
         WA_WQ4(wq4_layernorm(g.xd, L.ln3_w, L.ln3_b, rows, D, WQ4_PREC_F16X2, nullptr, g.hid, st));
         WA_WQ4(wq4_ffn_forward_ws(L.fc1, L.fc1_b, L.fc2, L.fc2_b, g.hid, g.xd, g.xd, rows, WQ4_EPI_RESIDUAL,
@@ -1131,7 +1157,7 @@ wq4_status ensure_graph(wa_model* m, DecGroup& g, int eot_stop) {
   // buffers, the range tier; one explicit field per mixed-radix digit
   const int64_t key =
       (((((int64_t)g.b0 * 512 + g.nb) * 2 + (eot_stop ? 1 : 0)) * 2 + (m->trace_out ? 1 : 0)) * 2 +
-       (m->group_kv(g) ? 1 : 0)) * 3 + (m->wide_ffn ? 2 : m->wide_range ? 1 : 0);
+       (m->group_kv(g) ? 1 : 0)) * 4 + m->range_tier();
   if (g.graph && g.graph_key == key) return WQ4_OK;
   if (g.graph) {
     (void)hipGraphExecDestroy(g.graph);
@@ -1171,11 +1197,24 @@ wq4_status ensure_ffn_ws(wa_model* m) {
   const size_t ne = wq4_ffn_workspace_bytes(Le.fc1, Le.fc2, (int64_t)m->bmax * m->cfg.n_audio_ctx);
   const size_t nd = wq4_ffn_workspace_bytes(Ld.fc1, Ld.fc2, (int64_t)m->bmax * 4);
   if (ne == 0 || nd == 0) return fail(WQ4_EINVAL, "FFN workspace size");
+  // all or nothing: a partial failure releases what it got, so a later
+  // tier-2 entry allocates (or fails) afresh instead of leaking the first set
   void* e = m->dev.alloc<uint8_t>(ne);
-  if (!e) return fail(WQ4_ENOMEM, "range tier 2: FFN workspace allocation failed");
+  bool ok = e != nullptr;
   for (DecGroup& g : m->groups) {
-    g.ffn_ws = m->dev.alloc<uint8_t>(nd);
-    if (!g.ffn_ws) return fail(WQ4_ENOMEM, "range tier 2: FFN workspace allocation failed");
+    g.ffn_ws = ok ? m->dev.alloc<uint8_t>(nd) : nullptr;
+    ok = ok && g.ffn_ws != nullptr;
+  }
+  if (!ok) {
+    m->dev.release(e);
+    for (DecGroup& g : m->groups) {
+      m->dev.release(g.ffn_ws);
+      g.ffn_ws = nullptr;
+      g.ffn_ws_bytes = 0;
+    }
+    return fail(WQ4_ENOMEM, "range tier 2: FFN workspace allocation failed");
+  }
+  for (DecGroup& g : m->groups) {
     g.ffn_ws_bytes = nd;
     m->bytes += nd;
   }
@@ -1594,13 +1633,20 @@ wq4_status transcribe_pipelined(wa_model* m, const float* mel_dev, int NB, int B
   int32_t* host = nullptr;
   const size_t per = (size_t)B * kMaxTokens + B + 1;
   WA_HIP(hipHostMalloc(reinterpret_cast<void**>(&host), (size_t)NB * per * 4, 0));
-  struct HostGuard {  // an early error return may leave copies into `p` queued: drain them first
+  struct HostGuard {  // an early error return may leave copies into `p` queued: drain this model's streams first
+    wa_model* m;
     int32_t* p;
+    bool done = false;  // success: the model stream was synchronised after the last copy
     ~HostGuard() {
-      (void)hipDeviceSynchronize();
+      if (!done) {
+        (void)hipStreamSynchronize(m->own_stream);
+        if (m->enc_stream) (void)hipStreamSynchronize(m->enc_stream);
+        for (DecGroup& g : m->groups)
+          if (g.st) (void)hipStreamSynchronize(g.st);
+      }
       (void)hipHostFree(p);
     }
-  } hg{host};
+  } hg{m, host};
   EventSet ev;
   struct Batch {
     hipEvent_t ready, mstart, mend, pstart, gprompt[kMaxGroups], gdone[kMaxGroups];
@@ -1626,7 +1672,11 @@ wq4_status transcribe_pipelined(wa_model* m, const float* mel_dev, int NB, int B
   if (s != WQ4_OK) return s;
   WA_HIP(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
   WA_HIP(hipEventRecord(bt[0].ready, st));
-  if (m->overlap_k < 0) m->overlap_k = std::min(L, kEncOverlapLayers0);
+  // the adapted depth belongs to a batch shape: a call with another clip
+  // count or EOT mode starts again from the default
+  if (m->overlap_k < 0 || m->overlap_b != B || m->overlap_eot != eot_stop) m->overlap_k = std::min(L, kEncOverlapLayers0);
+  m->overlap_b = B;
+  m->overlap_eot = eot_stop;
   double t_exposed = 0.0, t_masked = 0.0, t_decode = 0.0, t_prompt = 0.0, k_sum = 0.0;
   int32_t steps_all = 0;
   for (int i = 0; i < NB; ++i) {
@@ -1679,6 +1729,7 @@ wq4_status transcribe_pipelined(wa_model* m, const float* mel_dev, int NB, int B
     }
   }
   WA_HIP(hipStreamSynchronize(st));
+  hg.done = true;
   for (int i = 0; i < NB; ++i) {
     const int32_t* hb = host + (size_t)i * per;
     copy_tokens(hb, hb + (size_t)B * kMaxTokens, B, max_tokens, tokens_out + (size_t)i * B * max_tokens,
@@ -1753,10 +1804,19 @@ wq4_status wa_transcribe(wa_model* m, const float* mel_dev, int n_clips, int lan
                         &overflow);
     if (s != WQ4_OK) return s;
   }
+  if (overflow && !m->wide_attn) {
+    // an attention output feeds its output projection unnormalised: retry
+    // with f32 attention outputs and per-call operand scales on those
+    // projections (sticky; needs tier 2's workspaces, already allocated)
+    m->wide_attn = true;
+    s = transcribe_once(m, mel_dev, n_clips, lang_token, max_tokens, eot_stop, tokens_out, n_tokens_out, stream,
+                        &overflow);
+    if (s != WQ4_OK) return s;
+  }
   if (overflow)
     return fail(WQ4_ERANGE,
-                "activation overflow: an MFMA operand left the f16-pair range (|x| >= 4094 after the LayerNorm, "
-                "GELU or attention producers) and the logits are not finite");
+                "activation overflow: an MFMA operand left the f16-pair range (|x| >= 4094 after every range tier: "
+                "LayerNorm path, per-call FFN and attention-projection operand scales) and the logits are not finite");
   return WQ4_OK;
 }
 
@@ -1773,9 +1833,13 @@ wq4_status wa_transcribe_batches(wa_model* m, const float* mel_dev, int n_batche
                                       n_tokens_out, stream, flags.data());
   if (s != WQ4_OK) return s;
   const size_t mel_stride = (size_t)n_clips * m->cfg.n_mels * 2 * m->cfg.n_audio_ctx;
+  // the pipeline decoded every batch at the tier the model had on entry
+  const int tier0 = m->range_tier();
   for (int i = 0; i < n_batches; ++i) {
-    if (!flags[i]) continue;
-    // a flagged batch goes through wa_transcribe's range tiers on its own
+    // a flagged batch goes through wa_transcribe's range tiers on its own;
+    // once that raised the (sticky) tier, the later batches are re-run at it
+    // too -- one wa_transcribe per batch would have decoded them there
+    if (!flags[i] && m->range_tier() == tier0) continue;
     s = wa_transcribe(m, mel_dev + i * mel_stride, n_clips, lang_token, max_tokens, eot_stop,
                       tokens_out + (size_t)i * n_clips * max_tokens, n_tokens_out + (size_t)i * n_clips, stream);
     if (s != WQ4_OK) return s;
@@ -1789,7 +1853,7 @@ wq4_status wa_last_pipeline_stats(const wa_model* m, float* out) {
   return WQ4_OK;
 }
 
-int wa_model_wide_range(const wa_model* m) { return m ? (m->wide_ffn ? 2 : m->wide_range ? 1 : 0) : -1; }
+int wa_model_wide_range(const wa_model* m) { return m ? m->range_tier() : -1; }
 
 wq4_status wa_transcribe_trace(wa_model* m, const float* mel_dev, int n_clips, int lang_token, int max_tokens,
                                int eot_stop, int32_t* tokens_out, int32_t* n_tokens_out, const int32_t* trace_ids_dev,

@@ -34,6 +34,7 @@ namespace wa {
 namespace {
 
 using wq4::atile_store4;
+using wq4::attn_store4;
 using wq4::kbp_of;
 using wq4::split_f16;
 using wq4::half2v;
@@ -570,7 +571,8 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
                                                         const float* __restrict__ mlpart, int R, int H, int D, int S,
                                                         const uint8_t* __restrict__ wv,
                                                         const uint32_t* __restrict__ wvp,
-                                                        const float* __restrict__ bv, _Float16* __restrict__ tiled) {
+                                                        const float* __restrict__ bv, _Float16* __restrict__ tiled,
+                                                        float* __restrict__ out32) {
   // Zn of the RPW rows: f32 [column][row] (f16 weights, VALU projection) or
   // f16 hi / lo planes [row][column] (Q4 weights, MFMA projection)
   constexpr int ZLD = kMaxD + 8;  // halves; == 4 dwords (mod 64): conflict-free B fragment reads
@@ -774,7 +776,7 @@ __global__ __launch_bounds__(512) void xattn_out_kernel(const float* __restrict_
 #pragma unroll
     for (int g = 0; g < NPART; ++g) sacc += red[g][d][j] * (WK == kWtQ4 ? kOutInv : 1.0f);  // exact rescale
     const float v1 = __shfl_down(sacc, 1, 64), v2 = __shfl_down(sacc, 2, 64), v3 = __shfl_down(sacc, 3, 64);
-    if (r < R && (d & 3) == 0) atile_store4<NS>(tiled, r, h * 64 + 16 * mt0 + d, kbp_of(D), sacc, v1, v2, v3);
+    if (r < R && (d & 3) == 0) attn_store4<NS>(tiled, out32, D, r, h * 64 + 16 * mt0 + d, kbp_of(D), sacc, v1, v2, v3);
   }
 }
 
@@ -1062,26 +1064,27 @@ int out_rows(int R) {
 }
 template <int NS, int WK, int RPW>
 void launch_out_rpw(int R, int H, const float* z, const float* ml, int D, int S, const uint8_t* wv,
-                    const uint32_t* wvp, const float* bv, _Float16* tiled, hipStream_t st, bool split_outputs) {
+                    const uint32_t* wvp, const float* bv, _Float16* tiled, float* out32, hipStream_t st,
+                    bool split_outputs) {
   const dim3 go(H, (R + RPW - 1) / RPW);
   if constexpr (WK == kWtQ4) {
     if (split_outputs) {  // few rows: 4 workgroups per head
       hipLaunchKernelGGL((xattn_out_kernel<NS, WK, RPW, kXattnSplits, 4>), dim3(go.x, go.y, 4), dim3(512), 0, st, z,
-                         ml, R, H, D, S, wv, wvp, bv, tiled);
+                         ml, R, H, D, S, wv, wvp, bv, tiled, out32);
       return;
     }
   }
   hipLaunchKernelGGL((xattn_out_kernel<NS, WK, RPW, kXattnSplits, 1>), go, dim3(512), 0, st, z, ml, R, H, D, S, wv,
-                     wvp, bv, tiled);
+                     wvp, bv, tiled, out32);
 }
 template <int NS, int WK>
 void launch_out(int R, int H, const float* z, const float* ml, int D, int S, const uint8_t* wv, const uint32_t* wvp,
-                const float* bv, _Float16* tiled, hipStream_t st, bool split_outputs = false) {
+                const float* bv, _Float16* tiled, float* out32, hipStream_t st, bool split_outputs = false) {
   switch (out_rows(R)) {
-    case 1: launch_out_rpw<NS, WK, 1>(R, H, z, ml, D, S, wv, wvp, bv, tiled, st, split_outputs); break;
-    case 2: launch_out_rpw<NS, WK, 2>(R, H, z, ml, D, S, wv, wvp, bv, tiled, st, split_outputs); break;
-    case 8: launch_out_rpw<NS, WK, 8>(R, H, z, ml, D, S, wv, wvp, bv, tiled, st, split_outputs); break;
-    default: launch_out_rpw<NS, WK, 4>(R, H, z, ml, D, S, wv, wvp, bv, tiled, st, split_outputs); break;
+    case 1: launch_out_rpw<NS, WK, 1>(R, H, z, ml, D, S, wv, wvp, bv, tiled, out32, st, split_outputs); break;
+    case 2: launch_out_rpw<NS, WK, 2>(R, H, z, ml, D, S, wv, wvp, bv, tiled, out32, st, split_outputs); break;
+    case 8: launch_out_rpw<NS, WK, 8>(R, H, z, ml, D, S, wv, wvp, bv, tiled, out32, st, split_outputs); break;
+    default: launch_out_rpw<NS, WK, 4>(R, H, z, ml, D, S, wv, wvp, bv, tiled, out32, st, split_outputs); break;
   }
 }
 
@@ -1140,7 +1143,7 @@ hipError_t launch_wv_pack(const uint8_t* wv, int H, int D, uint32_t* out, hipStr
 
 hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, const uint32_t* wvp, const float* bv,
                         int wtype, const _Float16* enc, int B, int Tq, int T, int H, int D, _Float16* qt, float* part,
-                        _Float16* tiled, int ns, hipStream_t st) {
+                        _Float16* tiled, int ns, hipStream_t st, float* out32) {
   const int R = B * Tq;
   const int HT = (H + 15) / 16, HP = HT * 16;
   if (D != H * 64 || D % 128 != 0 || D > kMaxD || H > 20 || !q) return hipErrorInvalidValue;
@@ -1183,14 +1186,14 @@ hipError_t launch_xattn(const float* q, const uint8_t* wk, const uint8_t* wv, co
   // merge the splits and project with Wv into the output projection's operand
   if (wtype == kWtQ4) {
     if (ns == 2)
-      launch_out<2, kWtQ4>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, st, small);
+      launch_out<2, kWtQ4>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, out32, st, small);
     else
-      launch_out<1, kWtQ4>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, st, small);
+      launch_out<1, kWtQ4>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, out32, st, small);
   } else {
     if (ns == 2)
-      launch_out<2, kWtF16>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, st, small);
+      launch_out<2, kWtF16>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, out32, st, small);
     else
-      launch_out<1, kWtF16>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, st, small);
+      launch_out<1, kWtF16>(R, H, z, ml, D, p.splits, wv, wvp, bv, tiled, out32, st, small);
   }
   return hipGetLastError();
 }

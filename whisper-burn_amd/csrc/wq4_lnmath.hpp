@@ -67,6 +67,21 @@ __device__ __forceinline__ void atile_store4(_Float16* t, int row, int k, int kb
   if constexpr (NS == 2) *reinterpret_cast<half4*>(t + atile_index(row, k, kbp, NS, 1)) = lo;
 }
 
+// Attention-output store: four consecutive columns k .. k + 3 of row `row`
+// as the A-tiled operand of the output projection, or -- range tier 3
+// (wa_model: an attention output beyond the f16 pair's range) -- as f32 rows
+// [row][ld] into o32 when it is non-null (wave-uniform).
+template <int NS>
+__device__ __forceinline__ void attn_store4(_Float16* t, float* o32, int ld, int row, int k, int kbp, float a, float b,
+                                            float c, float d) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  if (o32) {
+    *reinterpret_cast<f4*>(o32 + (size_t)row * ld + k) = f4{a, b, c, d};
+    return;
+  }
+  atile_store4<NS>(t, row, k, kbp, a, b, c, d);
+}
+
 // LayerNorm-fold consumer: a row's mean and sqrt(var + eps) from its
 // `tiles` 16-column tile statistics (tile mean m_j, sum of squared
 // deviations q_j), spread over 16 consecutive lanes (part p holds tiles p,

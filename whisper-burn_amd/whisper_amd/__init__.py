@@ -302,7 +302,9 @@ class WhisperModel:
     @property
     def range_tier(self) -> int:
         """0 the product path, 1 the LayerNorm path, 2 the LayerNorm path with
-        every FFN on per-call operand scales (wa_model_wide_range)."""
+        every FFN on per-call operand scales, 3 also every attention output in
+        f32 with its output projection on per-call operand scales
+        (wa_model_wide_range)."""
         return lib().wa_model_wide_range(self._h)
 
     def device_bytes(self) -> int:
