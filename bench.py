@@ -100,6 +100,24 @@ def init_dist():
     return dist
 
 
+def baseline_config_label(variant: str, weights: str, precision: str, clips: int) -> str:
+    """Which BASELINE.json configuration this run is (configs 2-5), or why
+    it is none."""
+    if precision != "f16x2":
+        return "not a BASELINE config: f16 operands (--precision f16)"
+    if variant == "medium" and weights == "q4_0":
+        return "BASELINE config 2" + ("" if clips == 1 else f" at {clips} clips (config 2 is one clip)")
+    if variant == "large_v3" and weights == "f16":
+        return f"BASELINE config 5 (f16 weights), {clips} clip{'s' if clips != 1 else ''} per GPU"
+    if variant == "large_v3" and weights == "q4_0":
+        if clips == 1:
+            return "BASELINE config 3 (batch 1)"
+        if clips == 32:
+            return "BASELINE config 4 shard (32 of its 256 clips per GPU)"
+        return f"Large-V3 Q4_0 at {clips} clips per GPU (between BASELINE configs 3 and 4)"
+    return f"not a BASELINE config: {variant} {weights}"
+
+
 def job_rtf(world: int, B: int, steps: int, elapsed: float) -> float:
     """Whole-job real-time factor: audio seconds of all ranks' clips / wall s."""
     return world * B * steps * CLIP_SECONDS / elapsed
@@ -408,6 +426,9 @@ def main() -> None:
     ap.add_argument("--fixed-length", action="store_true", help="ignore EOT (always max-tokens steps)")
     ap.add_argument("--sequential", action="store_true",
                     help="one wa_transcribe per step (no encoder / decode pipelining across steps)")
+    ap.add_argument("--seq-steps", type=int, default=3,
+                    help="pipelined runs: batches then timed one wa_transcribe each, for value_sequential "
+                         "(0 = skip)")
     ap.add_argument("--cpu-rows", type=int, default=160,
                     help="rows the single-core CPU baseline times at M = 1500 (scaled to 1500)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -526,6 +547,22 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     model.profile_enable(False)
     prof = model.profile_read(reset=True)
+    # The same batches one wa_transcribe each (the reference's loop: one
+    # transcribe, encoder then decode, per call) -- reported beside the
+    # pipelined `value`, never as it.
+    seq_elapsed = None
+    n_seq = min(args.seq_steps, args.steps) if pipelined else 0
+    if n_seq > 0:
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        t2 = time.perf_counter()
+        for s in range(n_seq):
+            model.transcribe(inputs[args.warmup + s], lang, args.max_tokens, eot_stop=eot)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        seq_elapsed = max_over_ranks(time.perf_counter() - t2, dist, "cpu")
     # PCIe-inclusive figure (never `value`): one batch's inputs from pinned host
     # memory to HBM, timed after the timed steps and added per step
     host_in = inputs[0].cpu().pin_memory()
@@ -627,7 +664,8 @@ def main() -> None:
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp16x2" if prec == wq4.PREC_F16X2 else "fp16", "data": "synthetic",
             "config": {"workload": f"Whisper {args.variant} {args.weights.upper()}, {B} synthetic 30-s clips per GPU per step "
-                                   f"(BASELINE config 4 shard){', from audio' if args.audio else ''}, greedy KV-cached decode, max {args.max_tokens} "
+                                   f"({baseline_config_label(args.variant, args.weights, args.precision, B)})"
+                                   f"{', from audio' if args.audio else ''}, greedy KV-cached decode, max {args.max_tokens} "
                                    f"tokens, {'fixed length' if args.fixed_length else 'EOT stop'}",
                        "model": f"whisper-{args.variant.replace('_', '-')}-{args.weights} (synthetic weights)",
                        "global_batch": clips // args.steps, "seq_len": cfg["n_audio_ctx"],
@@ -652,6 +690,14 @@ def main() -> None:
             "input": "16 kHz audio in HBM (GPU log-mel timed)" if args.audio else "log-mel in HBM",
             "input_h2d_ms_per_step": round(h2d_s * 1e3, 3),
             "value_pcie_inclusive": round(job_rtf(world, B, args.steps, elapsed_pcie), 3),
+            "value_sequential": None if seq_elapsed is None else round(job_rtf(world, B, n_seq, seq_elapsed), 3),
+            "ms_per_step_sequential": None if seq_elapsed is None else round(seq_elapsed / n_seq * 1e3, 3),
+            "value_note": ("value: pipelined serving throughput (one wa_transcribe_batches call; the next batch's "
+                           "encoder beside the current decode); value_sequential: the same batches one "
+                           "wa_transcribe each, the reference's transcribe-per-call loop (whisper.rs:51-128) -- "
+                           "the like-for-like figure for the reference (BASELINE.md section 3); both with the "
+                           "mels resident in HBM, value_pcie_inclusive adds their H2D copy")
+            if pipelined else "one wa_transcribe per step (the reference's loop), mels resident in HBM",
             "log_mel_ms": round(float(np.mean(mel_ms)), 3) if mel_ms else None,
             "model_load_s": round(t_load, 2),
         }

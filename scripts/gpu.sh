@@ -9,6 +9,7 @@
 #   configs         BASELINE configs 2, 3, 5 (32 / 1 clip) and f16 precision
 #   trace           kernel trace of the bench's decode (BENCH_ARGS; 24 tokens):
 #                   tools/timeline.py, per-grid durations, in-graph xattn summary
+#   layers          kernel trace of the one-clip decode -> layer_table.txt (per-launch table of one layer)
 #   pmc             FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic.json
 #   stats           rocprofv3 --kernel-trace --stats of one bench step
 #   gemm            encoder GEMM kernels A/B (tools/enc_ab.py, ROWS list) + MFMA PMC
@@ -64,6 +65,14 @@ task_trace() {
   python3 scripts/in_graph_summary.py "$O/chain_grid.json" large_v3 q4_0 f16x2 32 "$O/xattn_in_graph.json" || return 1
   python3 scripts/decode_overlap.py "$f" large_v3 q4_0 f16x2 32 "$O/decode_overlap.json" > "$O/decode_overlap.log" || return 1
   cat "$O/timeline.txt" "$O/decode_overlap.log"
+  gzip -f "$f"
+}
+
+task_layers() {  # one-clip decode (BASELINE config 3): the per-launch table of one layer (tools/layer_table.py)
+  timeout -k 10 600 rocprofv3 --kernel-trace -d "$O/ltrace" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 \
+    --clips-per-gpu 1 --max-tokens 48 --fixed-length --no-cpu-baseline --seq-steps 0 > "$O/ltrace.log" 2>&1 || { tail "$O/ltrace.log"; return 1; }
+  local f; f=$(trace_csv "$O/ltrace")
+  python3 tools/layer_table.py "$f" "$O/layer_table.json" | tee "$O/layer_table.txt" || return 1
   gzip -f "$f"
 }
 
