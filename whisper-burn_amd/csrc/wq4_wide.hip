@@ -61,6 +61,42 @@ __device__ unsigned long long g_wide_stamps[kWideStampWgs * 2 * 6];
 #ifndef WQ4_WIDE_SCHED
 #define WQ4_WIDE_SCHED 2
 #endif
+// WQ4_WIDE_PRIO: waves 4-7 at s_setprio 1 for the whole kernel (A/B; off:
+// -4 to +2 %, profiles/r06_wide_prio_andor.log);
+// WQ4_WIDE_ANDOR (default on: +1-5 %, profiles/r06_wide_prio_andor.log): the
+// nibble dequantisation with v_and_or_b32 (one VALU
+// instruction per AND + OR pair; A/B).
+#ifndef WQ4_WIDE_PRIO
+#define WQ4_WIDE_PRIO 0
+#endif
+#ifndef WQ4_WIDE_ANDOR
+#define WQ4_WIDE_ANDOR 1
+#endif
+
+// deq8 (wq4_device.hpp) with each (w & mask) | C as one v_and_or_b32: the
+// same bits.
+__device__ __forceinline__ half8 deq8_andor(uint32_t w, uint32_t mlo, uint32_t mhi, uint32_t c) {
+  const uint32_t w8 = w >> 8;
+  uint32_t p0, p1, p2, p3;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(p0) : "v"(w), "s"(mlo), "v"(c));
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(p1) : "v"(w), "s"(mhi), "v"(c));
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(p2) : "v"(w8), "s"(mlo), "v"(c));
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(p3) : "v"(w8), "s"(mhi), "v"(c));
+  const half2v off1 = {(_Float16)1032.0f, (_Float16)1032.0f};
+  const half2v inv16 = {(_Float16)0.0625f, (_Float16)0.0625f};
+  const half2v off16 = {(_Float16)72.0f, (_Float16)72.0f};
+  const half2v h0 = __builtin_bit_cast(half2v, p0) - off1;
+  const half2v h1 = __builtin_bit_cast(half2v, p1) * inv16 - off16;
+  const half2v h2 = __builtin_bit_cast(half2v, p2) - off1;
+  const half2v h3 = __builtin_bit_cast(half2v, p3) * inv16 - off16;
+  half8 r;
+  r[0] = h0[0]; r[1] = h0[1];
+  r[2] = h1[0]; r[3] = h1[1];
+  r[4] = h2[0]; r[5] = h2[1];
+  r[6] = h3[0]; r[7] = h3[1];
+  return r;
+}
+
 // WQ4_WIDE_SPREAD (with WQ4_WIDE_SCHED 2): the next half step's LDS-DMA
 // copies issued one per MFMA chain (1) instead of all after the barrier (0).
 #ifndef WQ4_WIDE_SPREAD
@@ -150,6 +186,12 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
+  if (WQ4_WIDE_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half of each SIMD pair
+  // deq8_andor's constants: the masks in SGPRs, the OR constant in a VGPR
+  // (gfx9 VOP3 takes no literal and one SGPR)
+  const uint32_t kMaskLo = __builtin_amdgcn_readfirstlane(0x000F000Fu), kMaskHi = __builtin_amdgcn_readfirstlane(0x00F000F0u);
+  uint32_t kOrC = 0x64006400u;
+  asm volatile("" : "+v"(kOrC));
   const int r = lane & 31;
   const int ngroups = (ntiles + 7) / 8, mgroups = (mtiles + 7) / 8;
   const int wg = xcd_remap(blockIdx.x, ngroups * mgroups);
@@ -217,7 +259,9 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
     for (int nt = 0; nt < TN; ++nt) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
-        qf[nt][kk] = WQ4_WIDE_DIAG == 2 ? __builtin_bit_cast(half8, braw[nt]) : deq8(braw[nt][BLK * 2 + kk]);
+        qf[nt][kk] = WQ4_WIDE_DIAG == 2 ? __builtin_bit_cast(half8, braw[nt])
+                     : WQ4_WIDE_ANDOR ? deq8_andor(braw[nt][BLK * 2 + kk], kMaskLo, kMaskHi, kOrC)
+                                      : deq8(braw[nt][BLK * 2 + kk]);
       dsc[nt] = (float)__builtin_bit_cast(_Float16, (uint16_t)(BLK ? (bsc[nt] >> 16) : (bsc[nt] & 0xffffu)));
     }
     auto chain = [&](const half8 (&ah)[2], const half8 (&al)[2], int nt) {
