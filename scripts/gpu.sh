@@ -12,7 +12,10 @@
 #   layers          kernel trace of the one-clip decode -> layer_table.txt (per-launch table of one layer)
 #   pmc             FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic.json
 #   stats           rocprofv3 --kernel-trace --stats of one bench step
-#   gemm            encoder GEMM kernels A/B (tools/enc_ab.py, ROWS list) + MFMA PMC
+#   gemm            encoder GEMM kernels A/B (tools/enc_ab.py, ROWS_LIST, MODES 0 tile / 5 wide) + MFMA PMC
+#   gemmpmc         counter passes over the ring kernel and its timing builds
+#   widestamps      the wide kernel's K-loop phases and in-kernel clock (stamp build)
+#   gemmvariants    encoder-GEMM library variants in one process ($VARIANTS)
 #   groups          bench at WA_DECODE_GROUPS in $GLIST
 #   env             bench under each ';'-separated assignment list in $ENVLIST
 #   libs            bench with library variants whisper-burn_amd/diag/<v>/$LIB ($VARIANTS)
@@ -96,12 +99,12 @@ task_stats() {
 
 task_gemm() {
   for r in ${ROWS_LIST:-1500 48000}; do
-    ROWS=$r MODES=${MODES:-0,3} timeout -k 10 300 python -u tools/enc_ab.py > "$O/enc_ab_$r.log" 2>&1 || return 1
+    ROWS=$r MODES=${MODES:-0,5} timeout -k 10 300 python -u tools/enc_ab.py > "$O/enc_ab_$r.log" 2>&1 || return 1
     grep -v amdgpu.ids "$O/enc_ab_$r.log"
   done
   cd /tmp
-  ROWS=48000 MODES=0 ROUNDS=1 REPS=2 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
-    SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-include-regex "prefill|q4_gemm_enc" \
+  ROWS=48000 MODES=0,5 ROUNDS=1 REPS=2 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
+    SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-include-regex "prefill|q4_gemm_enc|wide" \
     -d "$ROOT/$O/gemm_pmc" -o run --output-format csv -- python3 "$ROOT/tools/enc_ab.py" > "$ROOT/$O/gemm_pmc.log" 2>&1 || { cd "$ROOT"; return 1; }
   cd "$ROOT"
   python3 scripts/mfma_summary.py "$O/gemm_pmc" | tee "$O/q4_gemm_mfma.txt"
@@ -130,6 +133,26 @@ task_gemmpmc() {
     done
   done
   cd "$ROOT"
+}
+
+# The wide kernel's K-loop phases (s_memtime / s_memrealtime stamps of
+# waves 0 and 4 per workgroup: vmcnt, barrier, LDS-DMA issue, compute, and
+# the in-kernel clock).  Needs the stamp build:
+#   make -C whisper-burn_amd variant V=stampw DEFS=-DWQ4_WIDE_STAMP=1
+task_widestamps() {
+  WQ4_LIB_DIR=whisper-burn_amd/diag/stampw timeout -k 10 300 python -u tools/wide_stamps.py > "$O/wide_stamps.log" 2>&1 || return 1
+  grep -v amdgpu.ids "$O/wide_stamps.log"
+}
+
+# Encoder-GEMM library variants timed in one process (tools/pf_variants.py):
+# lib/libwq4.so against whisper-burn_amd/diag/<v>/libwq4.so for v in
+# $VARIANTS (make -C whisper-burn_amd variant V=<v> DEFS=...), kernel mode
+# $ENC_MODE (5: the wide kernel), bit identity against the product reported.
+task_gemmvariants() {
+  local libs="whisper-burn_amd/lib/libwq4.so"
+  for v in $VARIANTS; do libs="$libs whisper-burn_amd/diag/$v/libwq4.so"; done
+  ENC_MODE=${ENC_MODE:-5} ROUNDS=${ROUNDS:-4} timeout -k 10 500 python -u tools/pf_variants.py $libs > "$O/gemm_variants.log" 2>&1 || return 1
+  grep -v amdgpu.ids "$O/gemm_variants.log"
 }
 
 task_groups() {
