@@ -21,9 +21,21 @@
  *    allocation inside the *_ws entry points (graph-capturable).  Distinct
  *    streams may be used concurrently from distinct host threads.
  *  - Result precision: products are formed from f16 hi/lo splits of the f32
- *    activations (x = hi + lo, both f16, ~22 significant bits) against the
- *    exact f16 value (q - 8) of each nibble, accumulated in f32 by MFMA; the
- *    per-block f16 scale is applied in f32 (see DESIGN.md "Numerics").
+ *    activations against the exact f16 value (q - 8) of each nibble,
+ *    accumulated in f32 by MFMA; the per-block f16 scale is applied in f32
+ *    (see DESIGN.md "Numerics").  The split is of x * s, s a power of two
+ *    (2^4 for the internal producers; at these f32 entry points picked per
+ *    call from max |x|: s = min(2^4, 2^floor(log2(16384 / max|x|)))), and
+ *    the MFMA flushes f16 subnormal inputs, so an element x carries
+ *      ~22 significant bits (x = hi + lo)  when |x s| >= 2^-3,
+ *      11 bits (hi alone: lo is an f16 subnormal) when 2^-14 <= |x s| < 2^-3,
+ *      nothing (flushed to 0)              when |x s| < 2^-14;
+ *    i.e. an absolute error floor of 2^-14 / s per element (2^-18 at s = 2^4)
+ *    below which the relative precision falls from 2^-22 to 2^-11.  In a dot
+ *    product the deficit is weighted by the small elements' share of
+ *    sum |x w| (tests/test_q4_gpu.py test_gelu_epilogue_vs_float64 holds an
+ *    identity-weight GEMM to exactly these terms).  WQ4_PREC_F16 keeps hi
+ *    only: 11 bits for every |x s| >= 2^-14.
  */
 #ifndef WQ4_H
 #define WQ4_H
