@@ -798,7 +798,11 @@ def test_f16_weights_out_of_decode_step_range(torch):
                                               (300, 1280, 5120, 2, 0), (2049, 1280, 1280, 1, 0), (16000, 1280, 1280, 2, 0),
                                               (4500, 5120, 1280, 5, 0), (200, 96, 160, 0, 0), (1000, 1312, 1280, 4, 0),
                                               (2049, 1280, 1280, 4, 0), (1500, 1280, 5120, 3, 0), (2000, 5120, 1280, 5, 1),
-                                              (300, 1312, 160, 4, 1)])
+                                              (300, 1312, 160, 4, 1),
+                                              # K loop lengths for the wide kernel's peeled first block pair,
+                                              # three-pair trips and 0-3 trailing pairs (nbp = K / 64: 1, 4, 5, 6, 7)
+                                              (600, 1280, 64, 1, 0), (500, 1280, 256, 0, 0), (900, 1280, 320, 2, 0),
+                                              (400, 1280, 384, 0, 1), (700, 1280, 448, 4, 0)])
 def test_enc_kernel_bit_identical(torch, m, n, k, flags, prec):
     """The encoder-size GEMM kernels -- the ring kernel (its geometries: 256 x
     256 with 8 waves, 64 x 128 and 32 x 256 with 4) and the 8-wave wide

@@ -36,9 +36,14 @@ def main():
         at = torch.empty(L.wq4_atiled_bytes(M, k, 0), dtype=torch.uint8, device="cuda")
         wq4.check(L.wq4_tile_activations(vp(x.data_ptr()), M, k, k, 0, vp(at.data_ptr()), at.numel(), st))
         y = torch.empty(M, n, device="cuda")
-        for _ in range(3):
+        ms = []
+        for _ in range(4):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
             wq4.check(L.wq4_gemm_tiled(t.handle, None, vp(at.data_ptr()), None, vp(y.data_ptr()), None, M, 0, 0, 1, st))
-        torch.cuda.synchronize()
+            e1.record()
+            torch.cuda.synchronize()
+            ms.append(e0.elapsed_time(e1))
         mg, ng = (-(-M // 32) + 7) // 8, (n // 32 + 7) // 8
         wgs = min(mg * ng, 4096)
         buf = (ctypes.c_ulonglong * (wgs * 12))()
@@ -52,6 +57,14 @@ def main():
                   f"compute {fr[3]:.3f}; {np.median(tot[:, w]) / halves:7.0f} cycles per half step "
                   f"(compute {np.median(a[:, w, 3]) / halves:6.0f}); clock {np.median(tot[:, w] / a[:, w, 5]) * 0.1:.2f} GHz",
                   flush=True)
+        # the whole launch against the K loops: rounds of one workgroup per CU
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        rounds = -(-mg * ng // cus)
+        loop_us = np.median(a[:, 0, 5]) * 0.01
+        kern_us = ms[-1] * 1e3
+        print(f"N={n:5d} K={k:5d} launch {kern_us:7.1f} us = {rounds} rounds x {kern_us / rounds:5.1f} us; "
+              f"K loop {loop_us:5.1f} us per workgroup (median), {kern_us / rounds - loop_us:5.1f} us per round outside it; "
+              f"{2 * M * n * k / (kern_us * 1e-6) / 1e12:6.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -49,7 +49,7 @@ namespace wq4 {
 #ifndef WQ4_WIDE_STAMP
 #define WQ4_WIDE_STAMP 0
 #endif
-constexpr int kWideStampWgs = 4096;
+[[maybe_unused]] constexpr int kWideStampWgs = 4096;
 #if WQ4_WIDE_STAMP
 __device__ unsigned long long g_wide_stamps[kWideStampWgs * 2 * 6];
 #endif
@@ -102,6 +102,15 @@ __device__ __forceinline__ half8 deq8_andor(uint32_t w, uint32_t mlo, uint32_t m
 #ifndef WQ4_WIDE_SPREAD
 #define WQ4_WIDE_SPREAD 1
 #endif
+// WQ4_WIDE_CARRY (with the pinned, spread schedule at NS = 2): no drain at a
+// half step's end -- the scale FMAs of its last two tiles ride behind the
+// next half step's first two chains (the temporaries rotate by two per half
+// step), and the next half step's first A fragments, nibbles and its
+// dequantisation are done under the last two chains, so a half step opens
+// straight into MFMAs.  The barrier at half step h then publishes slot h + 1.
+#ifndef WQ4_WIDE_CARRY
+#define WQ4_WIDE_CARRY 1
+#endif
 
 // One MFMA of a block chain, t = A B + (first ? 0 : t); nop: open with
 // s_nop 1 (the B operand may have been written by the VALU just before).
@@ -118,8 +127,17 @@ __device__ __forceinline__ void grp_mfma(floatx16& t, const half8& a, const half
 __device__ __forceinline__ void grp_mfma_fma(floatx16& t, const half8& a, const half8& b, bool first, bool nop,
                                              float& c0, float& c1, float& c2, float& c3, float u0, float u1,
                                              float u2, float u3, float d) {
-  (void)nop;
-  if (first)
+  if (first && nop)
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_mfma_f32_32x32x16_f16 %0, %5, %6, 0\n\t"
+        "v_fma_f32 %1, %7, %11, %1\n\t"
+        "v_fma_f32 %2, %8, %11, %2\n\t"
+        "v_fma_f32 %3, %9, %11, %3\n\t"
+        "v_fma_f32 %4, %10, %11, %4"
+        : "=&v"(t), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
+        : "v"(a), "v"(b), "v"(u0), "v"(u1), "v"(u2), "v"(u3), "v"(d));
+  else if (first)
     asm volatile(
         "v_mfma_f32_32x32x16_f16 %0, %5, %6, 0\n\t"
         "v_fma_f32 %1, %7, %11, %1\n\t"
@@ -156,6 +174,33 @@ struct WideGeo {
 __device__ __forceinline__ void glds4(const void* gsrc, void* lds_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
                                    (__attribute__((address_space(3))) void*)lds_base, 4, 0, 0);
+}
+
+// A raw buffer descriptor over `bytes` bytes at a wave-uniform base (the
+// inputs readfirstlane'd so hipcc keeps it in SGPRs, guide T8 / T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wide_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+// buffer LDS-DMA of `size` (4 / 16) bytes per lane: lane l's bytes land at
+// lds_base + size l (counted in vmcnt like global_load_lds).
+__device__ __forceinline__ void blds(__amdgpu_buffer_rsrc_t r, void* lds_base, int size, uint32_t voff,
+                                     uint32_t soff) {
+  if (size == 16)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_base, 16, voff, soff, 0, 0);
+  else
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_base, 4, voff, soff, 0, 0);
+}
+
+// This lane's id, recomputed at every call (volatile: never CSE'd into a
+// value hipcc keeps live across the K loop).
+__device__ __forceinline__ uint32_t fresh_lane() {
+  uint32_t l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
 }
 
 // s_waitcnt vmcnt(N), the other counters untouched (gfx9 encoding).
@@ -204,23 +249,37 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
   // copy those of 0-3 again, so every wave issues the same count); indices
   // are clamped to the last tile: the duplicate rows / columns are never
   // stored.
-  const uint8_t* asrc =
-      reinterpret_cast<const uint8_t*>(at) + (size_t)min(mg * 8 + wave, mtiles - 1) * nbp * CHUNK + lane * 16;
-  const int lnt = min(ng * 8 + wave, ntiles - 1);
-  const uint8_t* nsrc = nib + (size_t)lnt * nbp * 1024 + lane * 16;
-  const int snt = min(ng * 8 + 2 * (wave & 3) + (lane >> 5), ntiles - 1);
-  const uint8_t* ssrc = reinterpret_cast<const uint8_t*>(sc) + (size_t)snt * nbp * 128 + (lane & 31) * 4;
+  // The copies are buffer LDS-DMA loads: a descriptor per operand row in
+  // SGPRs, the half step's offset in soffset, one shared 32-bit per-lane
+  // voffset -- flat global_load_lds would keep 64-bit VGPR addresses live
+  // across the loop, which the carried schedule cannot afford.
+  const uint32_t abytes = (uint32_t)nbp * CHUNK, nbytes = (uint32_t)nbp * 1024;
+  const __amdgpu_buffer_rsrc_t arsrc =
+      wide_rsrc(reinterpret_cast<const uint8_t*>(at) + (size_t)min(mg * 8 + wave, mtiles - 1) * abytes, abytes);
+  const __amdgpu_buffer_rsrc_t nrsrc = wide_rsrc(nib + (size_t)min(ng * 8 + wave, ntiles - 1) * nbytes, nbytes);
+  // scales: lanes 32-63 copy the second n-tile of the wave's pair (voffset < 4 GiB: N K / 16 bytes)
+  const __amdgpu_buffer_rsrc_t srsrc = wide_rsrc(sc, (uint32_t)ntiles * nbp * 128);
+  const uint32_t lane16 = lane * 16;
+  // the scale copy's per-lane offset, rebuilt from a fresh lane id at each
+  // use (held in a VGPR across the loop, it is one too many for the carried
+  // schedule): lanes 32-63 copy the pair's second n-tile (clamped)
+  const int snt0 = min(ng * 8 + 2 * (wave & 3), ntiles - 1), snt1 = min(ng * 8 + 2 * (wave & 3) + 1, ntiles - 1);
+  const uint32_t sbase = (uint32_t)snt0 * nbp * 128, sdelta = (uint32_t)(snt1 - snt0) * nbp * 128;
+  auto soff = [&]() {
+    const uint32_t l = fresh_lane();
+    return sbase + (l >> 5) * sdelta + ((l & 31) << 2);
+  };
 
   // copy n (0 .. FR + 1) of half step h's CNT0 / CNT1 copies into its slot
   auto issue_part = [&](int h, int n) {
     const int bp = h >> 1, blk = h & 1;
     uint8_t* base = smem + (h >> 1 & 1) * G::PAIR + blk * (G::AH + G::BH);
     if (n < FR)
-      glds16(asrc + (size_t)bp * CHUNK + (blk * FR + n) * 1024, base + wave * (FR * 1024) + n * 1024);
+      blds(arsrc, base + wave * (FR * 1024) + n * 1024, 16, lane16, bp * CHUNK + (blk * FR + n) * 1024);
     else if (blk == 0 && n == FR)
-      glds16(nsrc + (size_t)bp * 1024, base + G::AH + wave * 1024);
+      blds(nrsrc, base + G::AH + wave * 1024, 16, lane16, bp * 1024);
     else if (blk == 0 && n == FR + 1)
-      glds4(ssrc + (size_t)bp * 128, base + G::AH + 8192 + wave * 256);
+      blds(srsrc, base + G::AH + 8192 + wave * 256, 4, soff(), bp * 128);
   };
   auto issue = [&](int h) {
 #pragma unroll
@@ -435,6 +494,186 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
 #else
 #define WIDE_STAMP(k)
 #endif
+  constexpr bool kCarry = WQ4_WIDE_CARRY && WQ4_WIDE_SCHED == 2 && WQ4_WIDE_SPREAD && NS == 2 && !WQ4_WIDE_DIAG;
+  if constexpr (kCarry) {
+    // WQ4_WIDE_CARRY.  Every wave computes, inactive ones (n-tiles past
+    // ntiles, partial last n-group only) on the clamped duplicate columns
+    // their epilogue never stores: no active / inactive branch in the loop,
+    // whose joins cost hipcc's allocator spills.
+    // State that lives across half steps -- the three
+    // temporaries (the last two tiles' FMAs are still owed), the next half
+    // step's dequantised nibbles, its first m-tile's A fragments and the
+    // block scales of this and the previous half step.
+    floatx16 tt[3];
+    half8 a[2][2];  // [kk][hi, lo] of one m-tile, each fragment replaced by the next m-tile's after its last MFMA
+    half8 qf[TN][2];
+    float dcur[TN], dprev[TN];
+#pragma unroll
+    for (int x = 0; x < 3; ++x)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) tt[x][i] = 0.0f;  // half step 0 "carries" fma(0, 0, +0) = +0 into acc[3][*]
+    dprev[0] = dprev[1] = 0.0f;
+    auto afrag = [&](const uint8_t* b, int mt, int kk, int q) {
+      return *reinterpret_cast<const half8*>(b + (wm * TM + mt) * (FR * 1024) + (kk * NS + q) * 1024 + lane * 16);
+    };
+    // the nibble words of ONE block (read just before their dequantisation)
+    // and the pair's scale word: 6 VGPRs fewer than holding the pair's
+    uint32_t bw[TN][2], bs[TN];
+    auto load_b = [&](const uint8_t* pb, int nt, int blk) {  // pb: the pair's even slot (still unrecycled)
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(pb + G::AH + (wn * TN + nt) * 1024 + lane * 16) + blk * 2;
+      bw[nt][0] = w[0];
+      bw[nt][1] = w[1];
+      bs[nt] = *reinterpret_cast<const uint32_t*>(pb + G::AH + 8192 + wn * 256 + nt * 128 + ((fresh_lane() & 31) << 2));
+    };
+    auto deq = [&](int nt) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) qf[nt][kk] = deq8_andor(bw[nt][kk], kMaskLo, kMaskHi, kOrC);
+    };
+    auto scale = [&](int nt, int blk) {
+      return (float)__builtin_bit_cast(_Float16, (uint16_t)(blk ? (bs[nt] >> 16) : (bs[nt] & 0xffffu)));
+    };
+    // One half step (block BLK of its pair) out of the slot at `base`, its
+    // temporaries rotated by OFF; nbase: the next half step's slot (next:
+    // there is one).  Tile j = (m-tile j / 2, n-tile j % 2) runs in
+    // tt[(j + OFF) % 3]; chains 0 / 1 carry the FMAs of the previous half
+    // step's tiles 6 / 7 (its OFF was OFF + 1 mod 3), chains j >= 2 those of
+    // tile j - 2.  Hazards as in the SCHED 2 path; chain 0 opens with s_nop
+    // 1 (its B operand was dequantised at the previous half step's end).
+    // mid_sync: the first half step, which runs without a barrier at its top
+    // (slot 0 was published by the prologue's), and so waits for and
+    // publishes slot 1 only before the chains that read it.
+    auto mid_sync = [&]() {
+      if (nbp > 1) vm_wait<G::CNT0 + G::CNT1>();  // only the copies of half steps 2 and 3 may be outstanding
+      else vm_wait<0>();
+      ring_barrier();
+    };
+    auto step = [&](const uint8_t* base, const uint8_t* nbase, auto blk_c, auto off_c, auto ms_c, int pend,
+                    bool next) __attribute__((always_inline)) {
+      constexpr int BLK = decltype(blk_c)::value, OFF = decltype(off_c)::value;
+      constexpr bool MS = decltype(ms_c)::value;
+#pragma unroll
+      for (int j = 0; j < 2 * TM; ++j) {
+        const int mt = j >> 1, nt = j & 1;
+        if (MS && j == 2 * TM - 2) mid_sync();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int kk = i >> 1, q = i & 1;
+          const int p = j >= 2 ? j - 2 : 6 + j;
+          floatx16& c = acc[p >> 1][p & 1];
+          const floatx16& t = tt[j >= 2 ? (p + OFF) % 3 : (j + OFF + 1) % 3];
+          const float d = j >= 2 ? dcur[p & 1] : dprev[j];
+          float c0 = c[4 * i], c1 = c[4 * i + 1], c2 = c[4 * i + 2], c3 = c[4 * i + 3];
+          grp_mfma_fma(tt[(j + OFF) % 3], a[kk][q], qf[nt][kk], i == 0, j == 0 && i == 0, c0, c1, c2, c3,
+                       t[4 * i], t[4 * i + 1], t[4 * i + 2], t[4 * i + 3], d);
+          c[4 * i] = c0;
+          c[4 * i + 1] = c1;
+          c[4 * i + 2] = c2;
+          c[4 * i + 3] = c3;
+          if (nt == 1) a[kk][q] = mt + 1 < TM ? afrag(base, mt + 1, kk, q) : afrag(nbase, 0, kk, q);
+          // the next half step's nibbles: the next pair's even slot, or this one's
+          if (j == 2 * TM - 2 && i >= 2) load_b(BLK ? nbase : base, i - 2, 1 - BLK);
+          if (i == 1 && j < FR + 2 && pend >= 0) issue_part(pend, j);  // one copy per chain
+        }
+        // the next half step's nibbles, each n-tile once its last chain here is issued
+        if (j >= 2 * TM - 2) deq(nt);
+      }
+      (void)next;  // the last half step prefetches from a valid slot too; its tiles 6 / 7 are finished after the loop
+#pragma unroll
+      for (int nt = 0; nt < TN; ++nt) {
+        dprev[nt] = dcur[nt];
+        dcur[nt] = scale(nt, 1 - BLK);
+      }
+    };
+    // the last half step's tiles 6 / 7 (its OFF = 2 (H - 1) mod 3)
+    auto finish = [&](auto off_c) {
+      constexpr int OFF = decltype(off_c)::value;
+      // the last chain's MFMA result is read by the VALU right behind it:
+      // pad the MFMA-write -> VALU-read window (18 states for 16 passes)
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(tt[(6 + OFF) % 3]), "+v"(tt[(7 + OFF) % 3]));
+#pragma unroll
+      for (int p = 2 * TM - 2; p < 2 * TM; ++p)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          acc[p >> 1][p & 1][e] = __builtin_fmaf(tt[(p + OFF) % 3][e], dprev[p & 1], acc[p >> 1][p & 1][e]);
+    };
+    // Ring protocol: the barrier at half step h publishes slot h + 1 (each
+    // wave has waited for its own copies of h + 1, only those of h + 2 may
+    // be outstanding) and frees slot h - 1 (read by half step h - 1 and by
+    // h - 2's prefetch), into which h's chains issue the copies of h + 3.
+    issue(0);
+    if (H > 1) issue(1);
+    if (H > 2) issue(2);
+    if (H > 2) vm_wait<G::CNT0 + G::CNT1>();
+    else vm_wait<G::CNT1>();
+    ring_barrier();
+    {
+#pragma unroll
+      for (int nt = 0; nt < TN; ++nt) {
+        load_b(smem, nt, 0);
+        deq(nt);
+        dcur[nt] = scale(nt, 0);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) a[kk][q] = afrag(smem, 0, kk, q);
+    }
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using NoMs = std::integral_constant<bool, false>;
+    // more_c: true when the caller knows a block pair follows (the loop
+    // body: no branch on it there)
+    auto pair = [&](int bp, auto offe, auto first_c, auto more_c) __attribute__((always_inline)) {
+      constexpr int OE = decltype(offe)::value, OO = (OE + 2) % 3;
+      constexpr bool FIRST = decltype(first_c)::value;
+      const bool more = decltype(more_c)::value || bp + 1 < nbp;
+      const uint8_t* b0 = smem + (bp & 1) * G::PAIR;
+      const uint8_t* b1 = b0 + G::AH + G::BH;
+      const uint8_t* bn = smem + ((bp + 1) & 1) * G::PAIR;
+      WIDE_STAMP(-1);
+      if constexpr (!FIRST) {
+        if (more) vm_wait<G::CNT0>();
+        else vm_wait<0>();
+        WIDE_STAMP(0);
+        ring_barrier();
+        WIDE_STAMP(1);
+      }
+      WIDE_STAMP(2);
+      step(b0, b1, I0{}, std::integral_constant<int, OE>{}, first_c, more ? 2 * bp + 3 : -1, true);
+      WIDE_STAMP(3);
+      if (more) vm_wait<G::CNT1>();
+      else vm_wait<0>();
+      WIDE_STAMP(0);
+      ring_barrier();
+      WIDE_STAMP(1);
+      WIDE_STAMP(2);
+      step(b1, bn, I1{}, std::integral_constant<int, OO>{}, NoMs{}, more ? 2 * bp + 4 : -1, more);
+      WIDE_STAMP(3);
+    };
+    // half step h runs with OFF = 2 h mod 3: even (2 bp) -> bp mod 3, odd ->
+    // bp + 2 mod 3.  The first pair is peeled (no barrier at its top), then
+    // three pairs per trip, so the rotation is straight code (a branch
+    // between the rotations costs hipcc's allocator ~1000 spilled VGPRs),
+    // then the last one to three pairs.
+    using Yes = std::integral_constant<bool, true>;
+    pair(0, I0{}, Yes{}, NoMs{});
+    int bp = 1;
+    for (; bp + 3 < nbp; bp += 3) {  // every pair here has a successor
+      pair(bp, I1{}, NoMs{}, Yes{});
+      pair(bp + 1, I2{}, NoMs{}, Yes{});
+      pair(bp + 2, I0{}, NoMs{}, Yes{});
+    }
+    if (bp < nbp) pair(bp, I1{}, NoMs{}, NoMs{});
+    if (bp + 1 < nbp) pair(bp + 1, I2{}, NoMs{}, NoMs{});
+    if (bp + 2 < nbp) pair(bp + 2, I0{}, NoMs{}, NoMs{});
+    {
+      const int ol = (2 * (H - 1)) % 3;
+      if (ol == 0) finish(std::integral_constant<int, 0>{});
+      else if (ol == 1) finish(std::integral_constant<int, 1>{});
+      else finish(std::integral_constant<int, 2>{});
+    }
+  } else {
   issue(0);
   if (H > 1) issue(1);
   if (H > 2) issue(2);
@@ -462,6 +701,7 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
     if (active) compute(b0 + G::AH + G::BH, std::integral_constant<int, 1>{}, 2 * bp + 4 < H ? 2 * bp + 4 : -1);
     else if (2 * bp + 4 < H) issue(2 * bp + 4);
     WIDE_STAMP(3);
+  }
   }
 #undef WIDE_STAMP
   __syncthreads();  // the ring is drained and read: the epilogue stage may reuse it
