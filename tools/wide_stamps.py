@@ -46,9 +46,10 @@ def main():
             ms.append(e0.elapsed_time(e1))
         mg, ng = (-(-M // 32) + 7) // 8, (n // 32 + 7) // 8
         wgs = min(mg * ng, 4096)
-        buf = (ctypes.c_ulonglong * (wgs * 12))()
+        buf = (ctypes.c_ulonglong * (wgs * 20))()
         got = L.wq4_diag_wide_stamps(buf, wgs)
-        a = np.frombuffer(buf, dtype=np.uint64).reshape(wgs, 2, 6).astype(np.float64)[:got]
+        raw = np.frombuffer(buf, dtype=np.uint64).reshape(wgs, 2, 10)[:got]
+        a = raw.astype(np.float64)
         tot = a[:, :, 4]
         halves = 2 * ((k // 32 + 1) // 2)
         for w, name in ((0, "wave 0"), (1, "wave 4")):
@@ -65,6 +66,22 @@ def main():
         print(f"N={n:5d} K={k:5d} launch {kern_us:7.1f} us = {rounds} rounds x {kern_us / rounds:5.1f} us; "
               f"K loop {loop_us:5.1f} us per workgroup (median), {kern_us / rounds - loop_us:5.1f} us per round outside it; "
               f"{2 * M * n * k / (kern_us * 1e-6) / 1e12:6.1f} TF/s", flush=True)
+        # workgroup lifetimes (wave 0, absolute 100 MHz ticks): entry -> K loop
+        # start -> K loop end -> epilogue stores complete; the CUs' occupancy
+        ent = raw[:, 0, 6].astype(np.int64)
+        end = raw[:, 0, 7].astype(np.int64)
+        lp = a[:, 0, 5]
+        life = (end - ent) * 0.01
+        span = (end.max() - ent.min()) * 0.01
+        if got == mg * ng:
+            print(f"N={n:5d} K={k:5d} workgroup life {np.median(life):6.1f} us median = K loop {np.median(lp) * 0.01:6.1f}"
+                  f" + the rest {np.median(life - lp * 0.01):5.1f} (prologue to loop + epilogue); "
+                  f"CU occupancy {life.sum() / (cus * span):.3f} over the {span:.0f}-us span", flush=True)
+            lend = raw[:, 0, 8].astype(np.int64)
+            iss = raw[:, 0, 9].astype(np.int64)
+            st0 = lend - (a[:, 0, 5]).astype(np.int64)
+            print(f"N={n:5d} K={k:5d}   entry -> loop {np.median(st0 - ent) * 0.01:5.1f} us, loop end -> epilogue issued "
+                  f"{np.median(iss - lend) * 0.01:5.1f} us, -> stores complete {np.median(end - iss) * 0.01:5.1f} us", flush=True)
 
 
 if __name__ == "__main__":

@@ -51,7 +51,7 @@ namespace wq4 {
 #endif
 [[maybe_unused]] constexpr int kWideStampWgs = 4096;
 #if WQ4_WIDE_STAMP
-__device__ unsigned long long g_wide_stamps[kWideStampWgs * 2 * 6];
+__device__ unsigned long long g_wide_stamps[kWideStampWgs * 2 * 10];
 #endif
 
 // WQ4_WIDE_SCHED: the half step's instruction order (A/B builds): 0 the
@@ -165,7 +165,9 @@ struct WideGeo {
   static constexpr int PAIR = 2 * AH + BH;          // slot 2p (A + B) then slot 2p + 1 (A)
   static constexpr int RING = 2 * PAIR;
   static constexpr int STAGE = 8 * 32 * kStageLd * 4;  // tiled epilogue stage (reuses the ring)
-  static constexpr int LDS = RING > STAGE ? RING : STAGE;
+  static constexpr int MAIN = RING > STAGE ? RING : STAGE;
+  // + the workgroup's 256 columns' colscale x act_inv and bias (tile_epilogue's `pre`)
+  static constexpr int LDS = MAIN + 2 * 256 * 4;
   static constexpr int CNT0 = FR + 2, CNT1 = FR;    // LDS-DMA copies per wave: even / odd half step
 };
 
@@ -224,6 +226,9 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
                                                               const _Float16* __restrict__ at, int mtiles, int nbp,
                                                               int ntiles, EpiArgs e) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+#if WQ4_WIDE_STAMP
+  const unsigned long long st_entry = __builtin_amdgcn_s_memrealtime();
+#endif
   using G = WideGeo<NS>;
   constexpr int TM = 4, TN = 2, FR = G::FR;
   constexpr int CHUNK = 4096 * NS;  // A bytes per (m-tile, block pair) in global memory
@@ -243,6 +248,23 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
   const int mg = wg / ngroups, ng = wg % ngroups;
   const int nt0 = ng * 8 + wn * TN;
   const bool active = nt0 < ntiles;  // wave-uniform (ntiles is even)
+  // The epilogue's per-column operands, staged in LDS while the K loop runs
+  // (loaded under the first copies, written before the first barrier): the
+  // epilogue starts without a memory round trip.  Thread t: column
+  // 256 ng + (t & 255), colscale (waves 0-3) or bias (waves 4-7).
+  float* pre = reinterpret_cast<float*>(smem + G::MAIN);
+  auto pre_load = [&]() {
+    const int col = ng * 256 + (tid & 255);
+    const bool isb = wave >= 4;
+    const uint32_t lim = isb ? (e.bias ? (uint32_t)e.n : 0u) : (uint32_t)ntiles * 32;
+    const __amdgpu_buffer_rsrc_t rs = isb ? wide_rsrc(e.bias, e.bias ? (uint32_t)e.n * 4 : 0)
+                                          : wide_rsrc(colscale, (uint32_t)ntiles * 128);
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)col < lim ? col * 4 : 0x80000000u, 0, 0));
+  };
+  auto pre_store = [&](float v) {
+    const float ainv = e.act_inv ? *e.act_inv : kActScaleInv;  // A operand scale (exact power of two)
+    pre[tid] = wave >= 4 ? v : v * ainv;
+  };
 
   // Loader role: wave w copies m-tile 8 mg + w, the nibbles of n-tile
   // 8 ng + w and the scales of n-tiles 8 ng + 2 (w & 3) + {0, 1} (waves 4-7
@@ -601,10 +623,12 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
     // be outstanding) and frees slot h - 1 (read by half step h - 1 and by
     // h - 2's prefetch), into which h's chains issue the copies of h + 3.
     issue(0);
+    const float pv = pre_load();  // lands with slot 0
     if (H > 1) issue(1);
     if (H > 2) issue(2);
     if (H > 2) vm_wait<G::CNT0 + G::CNT1>();
     else vm_wait<G::CNT1>();
+    pre_store(pv);
     ring_barrier();
     {
 #pragma unroll
@@ -704,18 +728,31 @@ __global__ __launch_bounds__(512, 1) void q4_gemm_wide_kernel(const uint8_t* __r
   }
   }
 #undef WIDE_STAMP
+  if constexpr (!kCarry) pre_store(pre_load());  // (the A/B path: after its loop)
   __syncthreads();  // the ring is drained and read: the epilogue stage may reuse it
 #if WQ4_WIDE_STAMP
   if (lane == 0 && (wave == 0 || wave == 4) && blockIdx.x < kWideStampWgs) {
-    unsigned long long* o = g_wide_stamps + ((size_t)blockIdx.x * 2 + (wave >> 2)) * 6;
+    unsigned long long* o = g_wide_stamps + ((size_t)blockIdx.x * 2 + (wave >> 2)) * 10;
     for (int k = 0; k < 4; ++k) o[k] = st_acc[k];
     o[4] = __builtin_amdgcn_s_memtime() - st_begin;
     o[5] = __builtin_amdgcn_s_memrealtime() - st_rbegin;  // 100 MHz ticks
+    o[6] = st_entry;
+    o[8] = __builtin_amdgcn_s_memrealtime();  // the K loop's end, absolute
   }
 #endif
 
   tile_epilogue<NS, EPI, TM, TN>(acc, mg * 8 + wm * TM, nt0, active, mtiles, colscale,
-                                 reinterpret_cast<float*>(smem) + wave * (32 * kStageLd), lane, e);
+                                 reinterpret_cast<float*>(smem) + wave * (32 * kStageLd), lane, e, pre + wn * TN * 32);
+#if WQ4_WIDE_STAMP
+  {
+    const unsigned long long issued = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0);  // the epilogue's stores completed
+    if (lane == 0 && (wave == 0 || wave == 4) && blockIdx.x < kWideStampWgs) {
+      g_wide_stamps[((size_t)blockIdx.x * 2 + (wave >> 2)) * 10 + 9] = issued;
+      g_wide_stamps[((size_t)blockIdx.x * 2 + (wave >> 2)) * 10 + 7] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+#endif
 }
 
 bool wide_gemm_supported(const Q4Geom& g, int rows, int ns, int wtype) {
@@ -751,12 +788,14 @@ hipError_t launch_wide_gemm(const Q4Geom& g, const uint8_t* nib, const uint32_t*
 }  // namespace wq4
 
 // Timing diagnostics (WQ4_WIDE_STAMP builds only; 0 workgroups otherwise):
-// copies [wgs][2 waves][6] loop-phase cycle sums of the last wide launch
-// (vmcnt, barrier, issue, compute, loop total; then the loop's s_memrealtime).
+// copies [wgs][2 waves][10] loop-phase cycle sums of the last wide launch
+// (vmcnt, barrier, issue, compute, loop total; then the loop's s_memrealtime,
+// the absolute s_memrealtime at kernel entry and after the epilogue's stores
+// completed; the K loop's end; the epilogue's last store issued).
 extern "C" int wq4_diag_wide_stamps(unsigned long long* out, int max_wgs) {
 #if WQ4_WIDE_STAMP
   const int n = max_wgs < wq4::kWideStampWgs ? max_wgs : wq4::kWideStampWgs;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(wq4::g_wide_stamps), (size_t)n * 2 * 6 * sizeof(unsigned long long)) !=
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(wq4::g_wide_stamps), (size_t)n * 2 * 10 * sizeof(unsigned long long)) !=
       hipSuccess)
     return -1;
   return n;
