@@ -93,6 +93,9 @@ task_stats() {
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/stats" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 \
     --no-cpu-baseline $BENCH_ARGS --json-out "$O/bench_under_rocprof.json" > "$O/stats.log" 2>&1 || return 1
   cp "$(ls "$O"/stats/*/run_kernel_stats.csv "$O"/stats/run_kernel_stats.csv 2>/dev/null | head -1)" "$O/kernel_stats.csv"
+  # the Q4 GEMM launches per queue: full width (what roofline_q4_gemm times) vs the CU-masked encoder stream
+  python3 scripts/kernel_by_queue.py "$(trace_csv "$O/stats")" "q4_gemm_wide|q4_gemm_prefill|q4_gemm_enc" \
+    "$O/q4_gemm_by_queue.json" | tee "$O/q4_gemm_by_queue.txt" || return 1
   rm -f "$(trace_csv "$O/stats")"
   python3 scripts/kstats.py "$O/kernel_stats.csv" 20
 }

@@ -17,6 +17,11 @@ constexpr int kStageLd = 68;  // padded f32 row stride of the transpose stage
 // voffset past any descriptor for masked columns (descriptors < 2 GiB, so
 // voffset + soffset cannot wrap).
 constexpr uint32_t kEpiOob = 0x80000000u;
+// cache-policy bits of the f32 epilogue's buffer stores (A/B builds only:
+// 0 = default, 2 = nt streaming)
+#ifndef WQ4_EPI_STORE_AUX
+#define WQ4_EPI_STORE_AUX 0
+#endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t epi_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
@@ -135,7 +140,7 @@ __device__ __forceinline__ void tile_epilogue(const floatx16 (&acc)[TM][TN], int
               for (int i = 0; i < 16; ++i)
                 __builtin_amdgcn_raw_buffer_store_b32(
                     __builtin_bit_cast(uint32_t, epi_value_pre(acc[m0 + mt][nt][i] * cs[nt], b[nt], res[mt][nt][i], e)),
-                    ro, voff[nt], soff(m0 + mt, i), 0);
+                    ro, voff[nt], soff(m0 + mt, i), WQ4_EPI_STORE_AUX);
         }
       } else {
 #pragma unroll
@@ -146,7 +151,7 @@ __device__ __forceinline__ void tile_epilogue(const floatx16 (&acc)[TM][TN], int
             for (int i = 0; i < 16; ++i)
               __builtin_amdgcn_raw_buffer_store_b32(
                   __builtin_bit_cast(uint32_t, epi_value_pre(acc[mt][nt][i] * cs[nt], b[nt], 0.0f, e)), ro, voff[nt],
-                  soff(mt, i), 0);
+                  soff(mt, i), WQ4_EPI_STORE_AUX);
       }
     } else if (active) {  // outputs past 2 GiB: pointer stores
 #pragma unroll
