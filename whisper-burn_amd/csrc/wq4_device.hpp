@@ -55,7 +55,10 @@ __device__ __forceinline__ float epi_value_pre(float acc, float bias, float res,
 // element's store -- y may alias residual (in-place residual adds) -- so the
 // tile paid 16 dependent memory round trips; this way it pays one.  Same
 // arithmetic as epi_value: the same bits.
-template <class RowOf, class Idx>
+// DRAIN: one vmcnt(0) after the loads, before the first store -- without it
+// hipcc re-waits (vmcnt(0), behind every earlier store) at the top of each
+// exec-masked store, i.e. per element (the encoder ring kernel's epilogue).
+template <bool DRAIN = false, class RowOf, class Idx>
 __device__ __forceinline__ void epi_store_tile(const floatx16& acc, float cs, int col, RowOf row_of, Idx idx,
                                                const EpiArgs& e) {
   const bool cok = col < e.n;
@@ -66,6 +69,7 @@ __device__ __forceinline__ void epi_store_tile(const floatx16& acc, float cs, in
     const int row = row_of(i);
     res[i] = (e.residual && cok && row < e.m) ? e.residual[(size_t)row * e.ldo + col] : 0.0f;
   }
+  if constexpr (DRAIN) __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int row = row_of(i);

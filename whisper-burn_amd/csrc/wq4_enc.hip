@@ -37,9 +37,11 @@
 
 #include <atomic>
 #include <cstdlib>
+#include <type_traits>
 
 #include "wq4_device.hpp"
 #include "wq4_kernels.hpp"
+#include "wq4_tile_epi.hpp"
 
 namespace wq4 {
 
@@ -298,69 +300,106 @@ __global__ __launch_bounds__(64 * WM * 4, WM == 2 ? 2 : 3) void q4_gemm_enc_kern
   const int nt0 = ng * G::NT + wc * TN;  // first n-tile of this wave
   float cs[TN];
   const float ainv = e.act_inv ? *e.act_inv : kActScaleInv;
+  // bias preloaded once (branch-free buffer loads): with no residual the
+  // epilogue then reads nothing, and hipcc has no load to drain vmcnt(0)
+  // for between the stores (it did so per element: wq4_tile_epi.hpp)
+  float b[TN];
+  {
+    const __amdgpu_buffer_rsrc_t rb = epi_rsrc(e.bias, e.bias ? (uint32_t)e.n * 4 : 0);
 #pragma unroll
-  for (int nt = 0; nt < TN; ++nt) cs[nt] = nt0 + nt < ntiles ? colscale[(nt0 + nt) * 32 + r] * ainv : 1.0f;
+    for (int nt = 0; nt < TN; ++nt) {
+      const int col = (nt0 + nt) * 32 + r;
+      cs[nt] = nt0 + nt < ntiles ? colscale[col] * ainv : 1.0f;
+      b[nt] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, col < e.n ? col * 4 : kEpiOob, 0, 0));
+    }
+    // landed before the first store: otherwise hipcc waits for them (vmcnt(0),
+    // behind every earlier store) at the top of each exec-masked store below
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  }
 
   if constexpr (EPI == kEpiF32 || EPI == kEpiHeadMajor) {
+    auto idx = [&](int row, int col) {
+      return EPI == kEpiHeadMajor ? out_index(e, row, col) : (size_t)row * e.ldo + col;
+    };
+    if (e.residual) {  // element-wise residual reads (all 16 of a tile before its stores)
 #pragma unroll
-    for (int mt = 0; mt < TM; ++mt)
+      for (int mt = 0; mt < TM; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < TN; ++nt)
-        epi_store_tile(
-            acc[mt][nt], cs[nt], (nt0 + nt) * 32 + r, [&](int i) { return (mt0 + mt) * 32 + acc_row_e(i, h); },
-            [&](int row, int col) {
-              return EPI == kEpiHeadMajor ? out_index(e, row, col) : (size_t)row * e.ldo + col;
-            },
-            e);
+        for (int nt = 0; nt < TN; ++nt)
+          epi_store_tile<true>(
+              acc[mt][nt], cs[nt], (nt0 + nt) * 32 + r, [&](int i) { return (mt0 + mt) * 32 + acc_row_e(i, h); },
+              idx, e);
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < TM; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < TN; ++nt) {
+          const int col = (nt0 + nt) * 32 + r;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int row = (mt0 + mt) * 32 + acc_row_e(i, h);
+            if (col < e.n && row < e.m) e.out[idx(row, col)] = epi_value_pre(acc[mt][nt][i] * cs[nt], b[nt], 0.0f, e);
+          }
+        }
+    }
   } else {
     static_assert(EPI == kEpiTiled, "f32, head-major f32 or A-tiled outputs");
     float* stage = reinterpret_cast<float*>(smem) + wave * (32 * kStageLdE);
     const size_t kbp_next = (size_t)e.nbp_next * 2;
     half8* dst = reinterpret_cast<half8*>(e.out_tiled);
+    // RES: residual reads element by element; without (the GELU GEMM) the
+    // preloaded bias and no memory read before the fragment stores
+    auto run = [&](auto res_c) {
+      constexpr bool RES = decltype(res_c)::value;
 #pragma unroll
-    for (int mt = 0; mt < TM; ++mt) {
+      for (int mt = 0; mt < TM; ++mt) {
 #pragma unroll
-      for (int nt = 0; nt < TN; ++nt)
+        for (int nt = 0; nt < TN; ++nt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int rl = acc_row_e(i, h);
-          const int row = (mt0 + mt) * 32 + rl;
-          const int col = (nt0 + nt) * 32 + r;
-          stage[rl * kStageLdE + nt * 32 + r] =
-              (row < e.m && col < e.n) ? epi_value(acc[mt][nt][i] * cs[nt], row, col, e) : 0.0f;
-        }
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's stage writes land before its reads
-      __builtin_amdgcn_wave_barrier();
-      // the slab as A-tiled fragments: lane (r, h) of (m-tile, n-tile = block
-      // of the next GEMM, kk) holds columns 16 kk + 8 h .. + 7 of row r
-      if ((mt0 + mt) < mtiles) {
+          for (int i = 0; i < 16; ++i) {
+            const int rl = acc_row_e(i, h);
+            const int row = (mt0 + mt) * 32 + rl;
+            const int col = (nt0 + nt) * 32 + r;
+            stage[rl * kStageLdE + nt * 32 + r] =
+                !(row < e.m && col < e.n) ? 0.0f
+                : RES                   ? epi_value(acc[mt][nt][i] * cs[nt], row, col, e)
+                                        : epi_value_pre(acc[mt][nt][i] * cs[nt], b[nt], 0.0f, e);
+          }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's stage writes land before its reads
+        __builtin_amdgcn_wave_barrier();
+        // the slab as A-tiled fragments: lane (r, h) of (m-tile, n-tile = block
+        // of the next GEMM, kk) holds columns 16 kk + 8 h .. + 7 of row r
+        if ((mt0 + mt) < mtiles) {
 #pragma unroll
-        for (int nt = 0; nt < TN; ++nt) {
-          if (nt0 + nt >= ntiles) continue;  // padding n-tiles (N % 64 == 32) are written: zeros
+          for (int nt = 0; nt < TN; ++nt) {
+            if (nt0 + nt >= ntiles) continue;  // padding n-tiles (N % 64 == 32) are written: zeros
 #pragma unroll
-          for (int kk = 0; kk < 2; ++kk) {
-            const float* src = stage + r * kStageLdE + nt * 32 + kk * 16 + h * 8;
-            const floatx4 a = *reinterpret_cast<const floatx4*>(src);
-            const floatx4 c = *reinterpret_cast<const floatx4*>(src + 4);
-            half8 hi, lo;
+            for (int kk = 0; kk < 2; ++kk) {
+              const float* src = stage + r * kStageLdE + nt * 32 + kk * 16 + h * 8;
+              const floatx4 a = *reinterpret_cast<const floatx4*>(src);
+              const floatx4 c = *reinterpret_cast<const floatx4*>(src + 4);
+              half8 hi, lo;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              _Float16 x, y;
-              split_act(a[j], x, y);
-              hi[j] = x;
-              lo[j] = y;
-              split_act(c[j], x, y);
-              hi[4 + j] = x;
-              lo[4 + j] = y;
+              for (int j = 0; j < 4; ++j) {
+                _Float16 x, y;
+                split_act(a[j], x, y);
+                hi[j] = x;
+                lo[j] = y;
+                split_act(c[j], x, y);
+                hi[4 + j] = x;
+                lo[4 + j] = y;
+              }
+              const size_t frag = (((size_t)(mt0 + mt) * kbp_next + (nt0 + nt)) * 2 + kk) * 2;
+              dst[(frag + 0) * 64 + lane] = hi;
+              dst[(frag + 1) * 64 + lane] = lo;
             }
-            const size_t frag = (((size_t)(mt0 + mt) * kbp_next + (nt0 + nt)) * 2 + kk) * 2;
-            dst[(frag + 0) * 64 + lane] = hi;
-            dst[(frag + 1) * 64 + lane] = lo;
           }
         }
+        __builtin_amdgcn_wave_barrier();
       }
-      __builtin_amdgcn_wave_barrier();
-    }
+    };
+    if (e.residual) run(std::true_type{});
+    else run(std::false_type{});
   }
 }
 

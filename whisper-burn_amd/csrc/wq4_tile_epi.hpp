@@ -93,6 +93,10 @@ __device__ __forceinline__ void tile_epilogue(const floatx16 (&acc)[TM][TN], int
       cs[nt] = active ? colscale[col] * ainv : 1.0f;
       b[nt] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, col < e.n ? col * 4 : kEpiOob, 0, 0));
     }
+    // landed before the first store (vmcnt(0) with nothing else in flight):
+    // otherwise hipcc waits for them, behind every earlier store, at the top
+    // of each exec-masked head-major store
+    __builtin_amdgcn_s_waitcnt(0x0F70);
   }
 
   if constexpr (EPI == kEpiF32) {
