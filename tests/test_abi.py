@@ -141,17 +141,18 @@ def test_precision_and_policy_setters():
 def test_gemm_kernel_name_follows_rows():
     """wq4_gemm_kernel_name (bench.py's roofline label): the decode-step kernel
     at <= 32 rows, the 8-wave decode kernel to 128, the encoder ring kernel at
-    one clip (M = 1500: the tile kernel's grid would leave CUs idle), the
-    8-wave wide kernel once its own grid has >= 400 workgroups (32 clips, M =
-    48000), the tile kernel between (M = 12000 at N = 1280: 235 wide
-    workgroups)."""
+    one clip (M = 1500: the tile kernel's grid would leave CUs idle) and up
+    to a wide grid of 170 workgroups, the 8-wave wide kernel from there (M =
+    12000 at N = 1280: 235 workgroups; 32 clips, M = 48000); the prefill tile
+    kernel under kernel policy 1 (and for operands the others do not take)."""
     assert wq4.gemm_kernel_name(1280, 1280, 16) == "skinny_gemm_kernel"
     assert wq4.gemm_kernel_name(1280, 1280, 100) == "q4_gemm_decode_kernel"
     assert wq4.gemm_kernel_name(1280, 1280, 1500) == "q4_gemm_enc_kernel"
     assert wq4.gemm_kernel_name(5120, 1280, 1500) == "q4_gemm_enc_kernel"
     assert wq4.gemm_kernel_name(1280, 1280, 48000) == "q4_gemm_wide_kernel"
     assert wq4.gemm_kernel_name(5120, 1280, 12000) == "q4_gemm_wide_kernel"
-    assert wq4.gemm_kernel_name(1280, 1280, 12000) == "q4_gemm_prefill_kernel"
+    assert wq4.gemm_kernel_name(1280, 1280, 12000) == "q4_gemm_wide_kernel"
+    assert wq4.gemm_kernel_name(1280, 1280, 6000) == "q4_gemm_enc_kernel"
     assert wq4.gemm_kernel_name(1280, 1281, 16) == ""
     wq4.set_kernel_policy(1)
     try:

@@ -425,8 +425,13 @@ static std::atomic<int> g_enc_mode{[] {
 // (profiles/r06_enc_ab_rows.log, tile vs wide interleaved in one process):
 // at M = 48000 the wide kernel is 1-7 % faster on every shape (457 / 454 /
 // 488 / 562 TF/s against 453 / 424 / 471 / 530), at 24000 and 12000 on 7 of
-// 8, at 6000 only where its own grid is >= 480 workgroups: wide while its
-// 256 x 256 grid has >= 400 workgroups.
+// 8, at 6000 only where its own grid is >= 480 workgroups.  After the wide
+// kernel's carried schedule and drain-free epilogue (profiles/r06ab_enc_ab_*.log,
+// r06aa_enc_ab_*.log, M = 3000 .. 24000, modes 0 / 2 / 3 / 5): the wide
+// kernel is fastest from ~170 of its workgroups up (+9-21 % where that moved
+// the choice: M = 3000 / N = 3840, 5120; M = 9000 / N = 1280; M = 12000 /
+// N = 1280), 3 % behind the tile kernel at M = 6000 / 9000, N = 3840 (a
+// third round of 256 workgroups 40 % full); below, the ring kernel's S.
 int enc_gemm_pick(const Q4Geom& g, int rows, int epi_mode, int ns, int wtype) {
   const int mode = g_enc_mode.load();
   if (mode == 0 || wtype != kWeightsQ4 || rows <= 128 || g.kb < 1) return 0;
@@ -434,7 +439,7 @@ int enc_gemm_pick(const Q4Geom& g, int rows, int epi_mode, int ns, int wtype) {
   const int64_t mt = round_up(rows, kMPad) / kMTile;
   const int64_t tile_grid = ((mt + 3) / 4) * ((g.ntiles + 7) / 8);
   const int64_t wide_grid = ((mt + 7) / 8) * ((g.ntiles + 7) / 8);
-  if (mode == 1 && wide_grid >= 400 && wide_gemm_supported(g, rows, ns, wtype)) return 5;
+  if (mode == 1 && wide_grid >= 170 && wide_gemm_supported(g, rows, ns, wtype)) return 5;
   if (ns != 2) return 0;  // the ring kernel: f16x2 operands only
   if (mode >= 2) return mode;
   return tile_grid < 400 ? 3 : 0;
