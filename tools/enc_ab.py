@@ -5,7 +5,11 @@ switched with wq4_debug_set_enc_kernel, on the four Large-V3 encoder shapes,
 interleaved over ROUNDS rounds on the same random operands.  Prints median /
 min ms and algorithmic TFLOP/s (2 M N K) per (shape, mode).
 
-    ROWS=48000 python tools/enc_ab.py      (env: ROWS, ROUNDS, REPS, MODES)
+    ROWS=48000 python tools/enc_ab.py      (env: ROWS, ROUNDS, REPS, MODES, FLAGS)
+
+FLAGS (the encoder's epilogues): 0 f32 rows, 2 + residual (in place: out and
+fc2), 5 GELU into the next GEMM's A-tiled operand (fc1), 1 | 4 alone as in
+test_enc_kernel_bit_identical.
 """
 import ctypes
 import os
@@ -26,6 +30,7 @@ ROUNDS = int(os.environ.get("ROUNDS", "5"))
 REPS = int(os.environ.get("REPS", "5"))
 MODES = [int(v) for v in os.environ.get("MODES", "0,2,3").split(",")]
 SHAPES = [(3840, 1280), (1280, 1280), (5120, 1280), (1280, 5120)]
+FLAGS = int(os.environ.get("FLAGS", "0"))
 
 
 def masked_stream(n):
@@ -59,17 +64,21 @@ def run_all():
         x = torch.randn(M, k, device="cuda")
         at = torch.empty(L.wq4_atiled_bytes(M, k, 0), dtype=torch.uint8, device="cuda")
         wq4.check(L.wq4_tile_activations(vp(x.data_ptr()), M, k, k, 0, vp(at.data_ptr()), at.numel(), st))
-        y = torch.empty(M, n, device="cuda")
-        setups.append((n, k, t, at, y))
+        y = torch.zeros(M, n, device="cuda")
+        ot = torch.empty(L.wq4_atiled_bytes(M, n, 0), dtype=torch.uint8, device="cuda") if FLAGS & 4 else None
+        setups.append((n, k, t, at, y, ot))
     torch.cuda.synchronize()
     times = {}
     prev = L.wq4_debug_set_enc_kernel(1)
     for _ in range(ROUNDS):
-        for si, (n, k, t, at, y) in enumerate(setups):
+        for si, (n, k, t, at, y, ot) in enumerate(setups):
             for mode in MODES:
                 L.wq4_debug_set_enc_kernel(mode)
-                run = lambda: wq4.check(L.wq4_gemm_tiled(t.handle, None, vp(at.data_ptr()), None, vp(y.data_ptr()), None,
-                                                         M, 0, 0, 1, st))
+                res = vp(y.data_ptr()) if FLAGS & 2 else None
+                out = None if FLAGS & 4 else vp(y.data_ptr())
+                tout = vp(ot.data_ptr()) if ot is not None else None
+                run = lambda: wq4.check(L.wq4_gemm_tiled(t.handle, None, vp(at.data_ptr()), res, out, tout,
+                                                         M, FLAGS, 0, 1, st))
                 run()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
@@ -82,7 +91,7 @@ def run_all():
     for si, (n, k, *_rest) in enumerate(setups):
         for mode in MODES:
             a = np.array(times[(si, mode)])
-            print(f"N={n:5d} K={k:5d} M={M} mode {mode}: median {np.median(a):.4f} ms min {a.min():.4f} "
+            print(f"N={n:5d} K={k:5d} M={M} flags {FLAGS} mode {mode}: median {np.median(a):.4f} ms min {a.min():.4f} "
                   f"-> {2 * M * n * k / np.median(a) / 1e9:7.1f} TF/s", flush=True)
 
 
