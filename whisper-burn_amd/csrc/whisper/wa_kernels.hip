@@ -20,6 +20,15 @@
 #include "../wq4_lnmath.hpp"
 #include "wa_kernels.hpp"
 
+// WA_LOGITS_NT (default on): the decode step's 266-MB embedding-table stream
+// (logits_argmax_f16_k32_kernel) with the nontemporal policy, so it does not
+// push the encoder planes the next step's cross-attention re-reads out of the
+// Infinity Cache: decode 928 -> 920 ms at 32 clips, RTF +0.7 % (two A/B runs
+// bracketed by the base build, profiles/r06af_libs.txt, r06ag_libs.txt).
+#ifndef WA_LOGITS_NT
+#define WA_LOGITS_NT 1
+#endif
+
 namespace wa {
 
 using wq4::floatx16;
@@ -1132,8 +1141,10 @@ __global__ __launch_bounds__(256) void logits_argmax_f16_k32_kernel(
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
         for (int p = 0; p < NS; ++p)  // D % kLg2Chunk == 0 (launcher): always in range
-          e[mt][ks][p] = *reinterpret_cast<const half8*>(er + (kc / kLg2Chunk) * chunk_halves +
-                                                          ((mt * KS + ks) * NS + p) * 512);
+          e[mt][ks][p] = WA_LOGITS_NT ? __builtin_nontemporal_load(reinterpret_cast<const half8*>(
+                                            er + (kc / kLg2Chunk) * chunk_halves + ((mt * KS + ks) * NS + p) * 512))
+                                      : *reinterpret_cast<const half8*>(er + (kc / kLg2Chunk) * chunk_halves +
+                                                                         ((mt * KS + ks) * NS + p) * 512);
   };
   // the hidden fragments of chunk c: A-tiled m-tile 0, blocks 4c .. 4c + 3
   // (kk, plane, lane: 1 KiB each, contiguous), staged through registers into
