@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "../wq4_device.hpp"
 #include "../wq4_lnmath.hpp"
@@ -76,6 +77,16 @@ constexpr int kXattnSplits = WA_XATTN_SPLITS;
 #ifndef WA_XATTN_DIAG
 #define WA_XATTN_DIAG 0
 #endif
+// Frames whose encoder-plane sub-chunks xattn_main loads with the default
+// cache policy; the rest use WA_XATTN_STREAM_AUX (nontemporal).  >= 1500:
+// all default (tuning builds: scripts/gpu.sh libs).
+#ifndef WA_XATTN_CACHE_FRAMES
+#define WA_XATTN_CACHE_FRAMES 1500
+#endif
+#ifndef WA_XATTN_STREAM_AUX
+#define WA_XATTN_STREAM_AUX 2
+#endif
+constexpr int kMaxFrames = 1500;
 // WA_XATTN_STAMP (tools/xattn_micro.hip only): the clock at the phase
 // boundaries of every sub-chunk of workgroup (0, 0), waves 0 and NW - 1,
 // into g_xstamp (read back with hipMemcpyFromSymbol; results unchanged).
@@ -337,13 +348,26 @@ __global__ __launch_bounds__(64 * NW) void xattn_main_kernel(const _Float16* __r
     row = rem / PPR;
     col = p * D + c0 + (rem - row * PPR) * 8;
   };
-  auto fetch = [&](u32x4v (&buf)[NLD], int chi) {
+  // Infinity Cache policy (WA_XATTN_CACHE_FRAMES): the sub-chunks of frames
+  // below the bound load with the default policy, the rest nontemporal, so
+  // that the part of every clip's planes that fits stays cached from one
+  // layer to the next instead of the whole set thrashing it (both decode
+  // groups' planes, 245 MB at 32 clips, against 256 MB).  Same values either
+  // way; one wave-uniform branch per sub-chunk.
+  auto fetch_aux = [&](u32x4v(&buf)[NLD], int chi, auto aux_c) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       int row, col;
       item(i, row, col);
-      buf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(((chi * kTc + row) * ROW + col) * 2), 0, 0);
+      buf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(((chi * kTc + row) * ROW + col) * 2), 0,
+                                                     decltype(aux_c)::value);
     }
+  };
+  auto fetch = [&](u32x4v (&buf)[NLD], int chi) {
+    if (WA_XATTN_CACHE_FRAMES >= kMaxFrames || ts + chi * kTc < WA_XATTN_CACHE_FRAMES)
+      fetch_aux(buf, chi, std::integral_constant<int, 0>{});
+    else
+      fetch_aux(buf, chi, std::integral_constant<int, WA_XATTN_STREAM_AUX>{});
   };
 
   // transposed-read lane geometry (Z phase): 16-lane group g reads rows
