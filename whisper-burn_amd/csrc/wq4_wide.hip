@@ -11,16 +11,22 @@
 //    wave 128 x 64 (4 x 2 tiles of 32 x 32): one workgroup per CU, two waves
 //    per SIMD, so one wave's block-scale FMAs and dequantisation issue beside
 //    its partner's MFMAs.
-//  * EVERY operand is staged by LDS-DMA (global_load_lds): the A fragments,
-//    the repacked nibbles and the block scales.  No ordinary global load in
-//    the K loop, so hipcc never drains vmcnt(0) there
-//    (cdna_hip_programming.md §5, "Projection GEMM at M = 256" item 4b).
+//  * EVERY operand is staged by LDS-DMA (buffer ..._lds loads through
+//    per-row descriptors): the A fragments, the repacked nibbles and the
+//    block scales.  No ordinary global load in the K loop, so hipcc never
+//    drains vmcnt(0) there (cdna_hip_programming.md §5, "Projection GEMM at
+//    M = 256" item 4b).
 //  * The K loop runs in half steps of one Q4 block (32 k) through a ring of
-//    four LDS slots: at the top of half step h each wave waits (counted
-//    vmcnt, never 0 in the loop) for its own copies of slot h, one raw
-//    s_barrier publishes them, then the copies of half step h + 3 are issued
-//    into the slot the barrier just freed -- three half steps stay in flight
-//    across the barrier ("Pipelining across barriers").
+//    four LDS slots; each wave waits with a counted vmcnt (never 0 in the
+//    loop) for its own copies, one raw s_barrier publishes them, and the
+//    copies of half step h + 3 are issued into the slot the barrier freed.
+//    In the product schedule (WQ4_WIDE_CARRY) the barrier at half step h
+//    publishes slot h + 1: the last two chains of h already read the next
+//    half step's first A fragments and nibbles, and the scale FMAs of h's
+//    last two tiles ride in h + 1's first chains -- no drain between half
+//    steps ("Pipelining across barriers").
+//  * Epilogue (wq4_tile_epi.hpp) without memory drains: column scales and
+//    bias staged in LDS during the loop, buffer stores masked by offset.
 //
 // LDS: slots 0 / 2 hold A (8 m-tiles x 2 NS KiB) + nibbles (8 n-tiles x 1
 // KiB, both blocks of the pair) + scales (8 n-tiles x 128 B, twice); slots
