@@ -107,7 +107,9 @@ __device__ __forceinline__ void tile_epilogue(const floatx16 (&acc)[TM][TN], int
     // Residuals of half the m-tiles in flight at once, all loaded before any
     // store of theirs (out may alias residual: same element, same lane).
     const uint64_t obytes = (uint64_t)e.m * (uint64_t)e.ldo * 4;
-    if (active && obytes < (1ull << 31)) {
+    // padded rows (< 256 past m) add to soffset: kEpiOob + soffset must not
+    // wrap past 2^32 back into the descriptor
+    if (active && obytes + (uint64_t)256 * (uint64_t)e.ldo * 4 < (1ull << 31)) {
       const __amdgpu_buffer_rsrc_t rr = epi_rsrc(e.residual, e.residual ? (uint32_t)obytes : 0);
       const __amdgpu_buffer_rsrc_t ro = epi_rsrc(e.out, (uint32_t)obytes);
       // element (mt, nt, i) at voff[nt] (this lane's column and row half h;
