@@ -793,6 +793,46 @@ def test_f16_weights_out_of_decode_step_range(torch):
         assert_q4_close(y, x.reshape(m, k), w.astype(np.float32), what=f"f16 |w| >= 256, policy {policy}")
 
 
+@pytest.mark.parametrize("flags", [0, 2])
+def test_enc_epilogue_past_2gib(torch, flags):
+    """An f32 output past 2 GiB (M = 110000 rows x N = 5120): the tile and
+    wide kernels' epilogue leaves its offset-masked buffer stores for the
+    pointer path (wq4_tile_epi.hpp), the ring kernel (its own epilogue) is the
+    reference -- bit-identical, with and without the in-place residual."""
+    import ctypes
+
+    m, n, k = 110000, 5120, 64
+    rng = np.random.default_rng(11 + flags)
+    q = oracle.quantize_convert_np((rng.standard_normal(n * k) * 0.05).astype(np.float32))
+    t = wq4.Q4Tensor.from_q4_bytes(q, [n, k])
+    L = wq4.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    p = lambda a: ctypes.c_void_p(a.data_ptr()) if a is not None else None  # noqa: E731
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    x = torch.randn(m, k, device="cuda:0", generator=g)
+    at = torch.zeros(L.wq4_atiled_bytes(m, k, 0), dtype=torch.uint8, device="cuda:0")
+    wq4.check(L.wq4_tile_activations(p(x), m, k, k, 0, p(at), at.numel(), st))
+    b = torch.randn(n, device="cuda:0", generator=g) * 0.1
+    res0 = torch.randn(m, n, device="cuda:0", generator=g) if flags & 2 else None
+    ref = None
+    prev = L.wq4_debug_set_enc_kernel(0)
+    try:
+        for mode in (3, 0, 5):
+            assert L.wq4_debug_set_enc_kernel(mode) >= 0
+            y = res0.clone() if flags & 2 else torch.full((m, n), 7.0, device="cuda:0")
+            wq4.check(L.wq4_gemm_tiled(t.handle, p(b), p(at), p(y) if flags & 2 else None, p(y), None, m, flags, 0, 1,
+                                       st))
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = y
+            else:
+                diff = int((y.view(torch.int32) != ref.view(torch.int32)).sum().item())
+                assert diff == 0, f"mode {mode}: {diff} of {y.numel()} outputs differ"
+                del y
+    finally:
+        L.wq4_debug_set_enc_kernel(prev)
+
+
 # ------------------------------- encoder GEMM: LDS-DMA ring kernel (wq4_enc.hip) --
 @pytest.mark.parametrize("m,n,k,flags,prec", [(1500, 1280, 1280, 0, 0), (3000, 3840, 1280, 0, 0), (700, 5120, 1280, 5, 0),
                                               (300, 1280, 5120, 2, 0), (2049, 1280, 1280, 1, 0), (16000, 1280, 1280, 2, 0),
